@@ -1,0 +1,136 @@
+/* qrkem -- MI355X-native batched post-quantum KEM engine: public C ABI.
+ *
+ * Built as quantum-resistant-p2p_amd/qrkem/libqrkem.so (hipcc, gfx950).
+ *
+ * Part 1 is the liboqs-compatible subset that the reference's vendored ctypes
+ * wrapper binds (quantum_resistant_p2p/vendor/oqs.py).  A maintainer can drop
+ * libqrkem.so in place of vendor/lib/linux/liboqs.so and the reference's own
+ * oqs.py loads it unchanged.  Part 2 adds the batched,
+ * stream-ordered, device-pointer entry points the reference has no equivalent
+ * for (it calls liboqs once per handshake on the asyncio thread).
+ *
+ * Ownership: callers allocate every output buffer (as oqs.py:316-317, 342-347,
+ * 369-371 do); the library owns only OQS_KEM handles, static strings and the
+ * device scratch inside a qrk_ctx.  Errors: OQS_SUCCESS (0) / OQS_ERROR (-1),
+ * as oqs.py:38-39; qrk_last_error() gives a message.
+ */
+#ifndef QRKEM_H
+#define QRKEM_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ *
+ * Part 1: liboqs-compatible subset                                    *
+ * ------------------------------------------------------------------ */
+
+typedef enum { OQS_ERROR = -1, OQS_SUCCESS = 0 } OQS_STATUS;
+
+/* Struct prefix read by oqs.py:241-253 (liboqs <= 0.12 layout): the wrapper
+ * reads method_name .. length_shared_secret and treats the three callbacks as
+ * opaque pointers. */
+typedef struct OQS_KEM {
+  const char *method_name;
+  const char *alg_version;
+  uint8_t claimed_nist_level;
+  bool ind_cca;
+  size_t length_public_key;
+  size_t length_secret_key;
+  size_t length_ciphertext;
+  size_t length_shared_secret;
+  OQS_STATUS (*keypair)(uint8_t *public_key, uint8_t *secret_key);
+  OQS_STATUS (*encaps)(uint8_t *ciphertext, uint8_t *shared_secret, const uint8_t *public_key);
+  OQS_STATUS (*decaps)(uint8_t *shared_secret, const uint8_t *ciphertext, const uint8_t *secret_key);
+} OQS_KEM;
+
+/* oqs.py:192 */
+void OQS_init(void);
+/* oqs.py:197-198 */
+const char *OQS_version(void);
+/* oqs.py:409 */
+size_t OQS_KEM_alg_count(void);
+/* oqs.py:397, 409 */
+const char *OQS_KEM_alg_identifier(size_t i);
+/* oqs.py:406 */
+int OQS_KEM_alg_is_enabled(const char *method_name);
+/* oqs.py:271, 396 -- NULL for unknown or not-enabled names */
+OQS_KEM *OQS_KEM_new(const char *method_name);
+/* oqs.py:318-322: host pointers, one handshake, randomness from the OS CSPRNG */
+OQS_STATUS OQS_KEM_keypair(const OQS_KEM *kem, uint8_t *public_key, uint8_t *secret_key);
+/* oqs.py:348-353 */
+OQS_STATUS OQS_KEM_encaps(const OQS_KEM *kem, uint8_t *ciphertext, uint8_t *shared_secret,
+                          const uint8_t *public_key);
+/* oqs.py:372-377 */
+OQS_STATUS OQS_KEM_decaps(const OQS_KEM *kem, uint8_t *shared_secret, const uint8_t *ciphertext,
+                          const uint8_t *secret_key);
+/* oqs.py:390 */
+void OQS_KEM_free(OQS_KEM *kem);
+/* oqs.py:386-389 */
+void OQS_MEM_cleanse(void *ptr, size_t len);
+
+/* Derandomised single-shot forms (names of liboqs >= 0.13's *_derand API):
+ * KeyGen coins = d||z (ML-KEM, 64 B) or s||seedSE||z (FrodoKEM); Encaps coins
+ * = m (32 B) or mu.  Host pointers. */
+OQS_STATUS OQS_KEM_keypair_derand(const OQS_KEM *kem, uint8_t *public_key, uint8_t *secret_key,
+                                  const uint8_t *seed);
+OQS_STATUS OQS_KEM_encaps_derand(const OQS_KEM *kem, uint8_t *ciphertext, uint8_t *shared_secret,
+                                 const uint8_t *public_key, const uint8_t *seed);
+
+/* ------------------------------------------------------------------ *
+ * Part 2: batched device API (no reference equivalent)                *
+ * ------------------------------------------------------------------ */
+
+typedef struct qrk_ctx qrk_ctx;
+
+/* One context per (process, device).  Holds device scratch, grown on demand. */
+int qrk_ctx_create(qrk_ctx **out, int device);
+void qrk_ctx_destroy(qrk_ctx *ctx);
+/* Handshakes per internal chunk (scratch = chunk * per-handshake bytes). */
+int qrk_ctx_set_chunk(qrk_ctx *ctx, size_t chunk);
+size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
+
+/* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */
+int qrk_kem_sizes(const char *alg, size_t out[6]);
+
+/* Batched operations.  ALL buffers are device pointers, contiguous AoS
+ * [n][len].  `coins` may be NULL (the library draws n*len bytes from the OS
+ * CSPRNG and uploads them); otherwise it is [n][keypair/encaps coin bytes].
+ * `status` (nullable, device int32[n]) receives -1 for encapsulation keys that
+ * fail the FIPS 203 section 7.2 modulus check, else 0.  `stream` is a
+ * hipStream_t (NULL = default stream).  Calls are stream-ordered and
+ * asynchronous; re-entrant across contexts. */
+int qrk_kem_keypair_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *pk, uint8_t *sk,
+                          const uint8_t *coins, void *stream);
+int qrk_kem_encaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ct, uint8_t *ss,
+                         const uint8_t *pk, const uint8_t *coins, int32_t *status, void *stream);
+int qrk_kem_decaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
+                         const uint8_t *sk, void *stream);
+
+/* Same, with host buffers (synchronous; copies through pinned staging). */
+int qrk_kem_keypair_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *pk, uint8_t *sk,
+                               const uint8_t *coins);
+int qrk_kem_encaps_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ct, uint8_t *ss,
+                              const uint8_t *pk, const uint8_t *coins, int32_t *status);
+int qrk_kem_decaps_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
+                              const uint8_t *sk);
+
+/* Bench inputs generated on device: out_i = SHAKE256("qrk-bench"||LE64(seed)||LE64(first+i), len),
+ * len a multiple of 8, <= 136.  Device pointer. */
+int qrk_bench_coins(qrk_ctx *ctx, size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t *out,
+                    void *stream);
+/* Flip one ciphertext bit per selected index (mode 0 none, 1 all, 2 Bernoulli(1/2)):
+ * h_i = SHAKE256("qrk-tamper"||LE64(seed)||LE64(i))[0..8), bit (h_i>>1) mod 8*ctlen. */
+int qrk_tamper(qrk_ctx *ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t *ct, void *stream);
+
+const char *qrk_last_error(void);
+int qrk_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QRKEM_H */

@@ -1,0 +1,468 @@
+// C ABI of libqrkem.so (declared in include/qrkem.h).
+//
+// Part 1 mirrors the liboqs entry points bound by the reference's ctypes
+// wrapper (quantum_resistant_p2p/vendor/oqs.py:192-198, 271, 318, 348, 372,
+// 386-390, 397, 406-411); each single-shot call is a batch of one on the GPU.
+// Part 2 is the batched device API.  There is no CPU fallback: with no HIP
+// device every KEM call returns OQS_ERROR and qrk_last_error() says why.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+
+#include "../../include/qrkem.h"
+#include "qrkem_internal.h"
+
+namespace qrk {
+
+// ------------------------------------------------------------------ algorithm table
+static AlgInfo ALGS[] = {
+    // name, family, level, k/n, pk, sk, ct, ss, kp coins, enc coins, aes, enabled
+    {"ML-KEM-512", Family::MLKEM, 1, 2, 800, 1632, 768, 32, 64, 32, false, true},
+    {"ML-KEM-768", Family::MLKEM, 3, 3, 1184, 2400, 1088, 32, 64, 32, false, true},
+    {"ML-KEM-1024", Family::MLKEM, 5, 4, 1568, 3168, 1568, 32, 64, 32, false, true},
+    {"FrodoKEM-640-AES", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, true, false},
+    {"FrodoKEM-640-SHAKE", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, false, false},
+    {"FrodoKEM-976-AES", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, true, false},
+    {"FrodoKEM-976-SHAKE", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, false, false},
+    {"FrodoKEM-1344-AES", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, true, false},
+    {"FrodoKEM-1344-SHAKE", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, false, false},
+};
+static const int NALG = (int)(sizeof(ALGS) / sizeof(ALGS[0]));
+
+// Names liboqs supports that this engine does not implement (listed so that
+// OQS_KEM_alg_is_enabled answers 0 rather than the name being unknown, the
+// distinction oqs.py:265-269 draws between MechanismNotEnabledError and
+// MechanismNotSupportedError).
+static const char* UNIMPLEMENTED[] = {"HQC-128", "HQC-192", "HQC-256"};
+static const int NUNIMPL = 3;
+
+const AlgInfo* find_alg(const char* name) {
+  if (!name) return nullptr;
+  for (int i = 0; i < NALG; ++i)
+    if (!strcmp(ALGS[i].name, name)) return &ALGS[i];
+  return nullptr;
+}
+int alg_count() { return NALG; }
+const AlgInfo* alg_at(int i) { return (i >= 0 && i < NALG) ? &ALGS[i] : nullptr; }
+
+}  // namespace qrk
+
+using namespace qrk;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+static int hip_fail(const char* what, hipError_t e) {
+  return fail(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------ context
+struct qrk_ctx {
+  int device = 0;
+  size_t chunk = 1 << 16;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  uint8_t* dstage = nullptr;  // device staging for host-pointer calls and generated coins
+  size_t dstage_bytes = 0;
+  uint8_t* hstage = nullptr;  // pinned host staging
+  size_t hstage_bytes = 0;
+  std::mutex mu;
+};
+
+static int ensure_device(int device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return fail("no HIP device available (libqrkem has no CPU path)");
+  if (device < 0 || device >= count) return fail("invalid device index");
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  return 0;
+}
+
+static int grow_device(void** p, size_t* have, size_t need, hipStream_t st) {
+  if (*have >= need) return 0;
+  if (*p) {
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+  }
+  hipError_t e = hipMalloc(p, need);
+  if (e != hipSuccess) return hip_fail("hipMalloc", e);
+  *have = need;
+  return 0;
+}
+
+static int grow_pinned(uint8_t** p, size_t* have, size_t need) {
+  if (*have >= need) return 0;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *have = 0;
+  hipError_t e = hipHostMalloc((void**)p, need, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail("hipHostMalloc", e);
+  *have = need;
+  return 0;
+}
+
+static int os_random(uint8_t* out, size_t n) {
+  while (n) {
+    ssize_t r = getrandom(out, n, 0);
+    if (r < 0) return fail("getrandom failed");
+    out += r;
+    n -= (size_t)r;
+  }
+  return 0;
+}
+
+static size_t scratch_for(const AlgInfo& a, size_t chunk) {
+  return a.family == Family::MLKEM ? mlkem_scratch_bytes(a, chunk) : frodo_scratch_bytes(a, chunk);
+}
+
+static const AlgInfo* resolve(const char* alg) {
+  const AlgInfo* a = find_alg(alg);
+  if (!a) {
+    fail(std::string("unsupported KEM: ") + (alg ? alg : "(null)"));
+    return nullptr;
+  }
+  if (!a->enabled) {
+    fail(std::string("KEM not enabled in this build: ") + alg);
+    return nullptr;
+  }
+  return a;
+}
+
+enum class Op { KEYPAIR, ENCAPS, DECAPS };
+
+// Core batched driver over device pointers, chunked.
+static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
+                     const uint8_t* i2, int32_t* status, hipStream_t st) {
+  if (n == 0) return 0;
+  if (ensure_device(ctx->device)) return -1;
+  const size_t chunk = std::min(ctx->chunk, n);
+  if (grow_device(&ctx->scratch, &ctx->scratch_bytes, scratch_for(a, chunk), st)) return -1;
+  // coins: NULL -> OS CSPRNG, uploaded to device staging
+  const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
+  const size_t clen = (op == Op::KEYPAIR) ? a.kp_coins : a.enc_coins;
+  bool synth = false;
+  if (op != Op::DECAPS && coins == nullptr) {
+    const size_t bytes = n * clen;
+    if (grow_pinned(&ctx->hstage, &ctx->hstage_bytes, bytes)) return -1;
+    if (grow_device((void**)&ctx->dstage, &ctx->dstage_bytes, bytes, st)) return -1;
+    (void)hipStreamSynchronize(st);  // pinned staging may still feed an earlier copy
+    if (os_random(ctx->hstage, bytes)) return -1;
+    hipError_t e = hipMemcpyAsync(ctx->dstage, ctx->hstage, bytes, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail("hipMemcpyAsync(coins)", e);
+    coins = ctx->dstage;
+    synth = true;
+  }
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t m = std::min(chunk, n - off);
+    hipError_t e = hipSuccess;
+    if (a.family == Family::MLKEM) {
+      switch (op) {
+        case Op::KEYPAIR:
+          e = mlkem_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, st);
+          break;
+        case Op::ENCAPS:
+          e = mlkem_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
+                           status ? status + off : nullptr, ctx->scratch, st);
+          break;
+        case Op::DECAPS:
+          e = mlkem_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, st);
+          break;
+      }
+    } else {
+      switch (op) {
+        case Op::KEYPAIR:
+          e = frodo_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, st);
+          break;
+        case Op::ENCAPS:
+          e = frodo_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
+                           ctx->scratch, st);
+          break;
+        case Op::DECAPS:
+          e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, st);
+          break;
+      }
+    }
+    if (e != hipSuccess) return hip_fail("kernel launch", e);
+  }
+  if (synth) {
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+  }
+  return 0;
+}
+
+// Host-pointer wrapper: stage inputs, run, copy outputs back, synchronise.
+static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2,
+                          const uint8_t* i1, const uint8_t* i2, int32_t* status) {
+  if (n == 0) return 0;
+  if (ensure_device(ctx->device)) return -1;
+  size_t l_o1, l_o2, l_i1, l_i2;
+  switch (op) {
+    case Op::KEYPAIR: l_o1 = a.pk, l_o2 = a.sk, l_i1 = i1 ? a.kp_coins : 0, l_i2 = 0; break;
+    case Op::ENCAPS: l_o1 = a.ct, l_o2 = a.ss, l_i1 = a.pk, l_i2 = i2 ? a.enc_coins : 0; break;
+    default: l_o1 = a.ss, l_o2 = 0, l_i1 = a.ct, l_i2 = a.sk; break;
+  }
+  const size_t l_st = status ? sizeof(int32_t) : 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_o1 = al(n * l_o1), b_o2 = al(n * l_o2), b_i1 = al(n * l_i1), b_i2 = al(n * l_i2),
+               b_st = al(n * l_st);
+  uint8_t* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, b_o1 + b_o2 + b_i1 + b_i2 + b_st + 256);
+  if (e != hipSuccess) return hip_fail("hipMalloc(stage)", e);
+  uint8_t *d_o1 = d, *d_o2 = d_o1 + b_o1, *d_i1 = d_o2 + b_o2, *d_i2 = d_i1 + b_i1, *d_st = d_i2 + b_i2;
+  hipStream_t st = nullptr;
+  int rc = 0;
+  if (l_i1) e = hipMemcpy(d_i1, i1, n * l_i1, hipMemcpyHostToDevice);
+  if (e == hipSuccess && l_i2) e = hipMemcpy(d_i2, i2, n * l_i2, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    rc = hip_fail("hipMemcpy(H2D)", e);
+  } else {
+    rc = run_batch(ctx, a, op, n, d_o1, l_o2 ? d_o2 : nullptr, l_i1 ? d_i1 : nullptr, l_i2 ? d_i2 : nullptr,
+                   status ? (int32_t*)d_st : nullptr, st);
+    if (!rc) {
+      e = hipStreamSynchronize(st);
+      if (e == hipSuccess) e = hipMemcpy(o1, d_o1, n * l_o1, hipMemcpyDeviceToHost);
+      if (e == hipSuccess && l_o2) e = hipMemcpy(o2, d_o2, n * l_o2, hipMemcpyDeviceToHost);
+      if (e == hipSuccess && status) e = hipMemcpy(status, d_st, n * l_st, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) rc = hip_fail("kernel execution / D2H", e);
+    }
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+// ------------------------------------------------------------------ default context (single-shot API)
+static std::mutex g_default_mu;
+static qrk_ctx* g_default = nullptr;
+
+static qrk_ctx* default_ctx() {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  if (!g_default) {
+    g_default = new qrk_ctx();
+    const char* dev = getenv("QRK_DEVICE");
+    g_default->device = dev ? atoi(dev) : 0;
+    g_default->chunk = 1 << 12;
+  }
+  return g_default;
+}
+
+static OQS_STATUS single(const AlgInfo& a, Op op, uint8_t* o1, uint8_t* o2, const uint8_t* i1, const uint8_t* i2) {
+  qrk_ctx* ctx = default_ctx();
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  int32_t status = 0;
+  int rc = run_batch_host(ctx, a, op, 1, o1, o2, i1, i2, op == Op::ENCAPS ? &status : nullptr);
+  if (rc == 0 && status != 0) rc = fail("encapsulation key failed the FIPS 203 modulus check");
+  return rc == 0 ? OQS_SUCCESS : OQS_ERROR;
+}
+
+// per-algorithm callbacks stored in OQS_KEM (liboqs semantics: no kem argument)
+template <int I>
+static OQS_STATUS cb_keypair(uint8_t* pk, uint8_t* sk) {
+  return single(ALGS[I], Op::KEYPAIR, pk, sk, nullptr, nullptr);
+}
+template <int I>
+static OQS_STATUS cb_encaps(uint8_t* ct, uint8_t* ss, const uint8_t* pk) {
+  return single(ALGS[I], Op::ENCAPS, ct, ss, pk, nullptr);
+}
+template <int I>
+static OQS_STATUS cb_decaps(uint8_t* ss, const uint8_t* ct, const uint8_t* sk) {
+  return single(ALGS[I], Op::DECAPS, ss, nullptr, ct, sk);
+}
+
+template <int I>
+static void fill_cbs(OQS_KEM* k, int idx) {
+  if constexpr (I < 9) {
+    if (idx == I) {
+      k->keypair = cb_keypair<I>;
+      k->encaps = cb_encaps<I>;
+      k->decaps = cb_decaps<I>;
+      return;
+    }
+    fill_cbs<I + 1>(k, idx);
+  }
+}
+
+extern "C" {
+
+// ------------------------------------------------------------------ Part 1: liboqs subset
+void OQS_init(void) {}
+
+const char* OQS_version(void) { return "0.12.0-qrkem-gfx950"; }
+
+size_t OQS_KEM_alg_count(void) { return (size_t)(NALG + NUNIMPL); }
+
+const char* OQS_KEM_alg_identifier(size_t i) {
+  if (i < (size_t)NALG) return ALGS[i].name;
+  if (i < (size_t)(NALG + NUNIMPL)) return UNIMPLEMENTED[i - NALG];
+  return nullptr;
+}
+
+int OQS_KEM_alg_is_enabled(const char* method_name) {
+  const AlgInfo* a = find_alg(method_name);
+  return a && a->enabled ? 1 : 0;
+}
+
+OQS_KEM* OQS_KEM_new(const char* method_name) {
+  const AlgInfo* a = find_alg(method_name);
+  if (!a || !a->enabled) return nullptr;
+  OQS_KEM* k = (OQS_KEM*)calloc(1, sizeof(OQS_KEM));
+  if (!k) return nullptr;
+  k->method_name = a->name;
+  k->alg_version = a->family == Family::MLKEM ? "FIPS203 (qrkem gfx950)" : "FrodoKEM round 3 (qrkem gfx950)";
+  k->claimed_nist_level = (uint8_t)a->level;
+  k->ind_cca = true;
+  k->length_public_key = a->pk;
+  k->length_secret_key = a->sk;
+  k->length_ciphertext = a->ct;
+  k->length_shared_secret = a->ss;
+  fill_cbs<0>(k, (int)(a - ALGS));
+  return k;
+}
+
+static const AlgInfo* alg_of(const OQS_KEM* kem) {
+  if (!kem) {
+    fail("null OQS_KEM");
+    return nullptr;
+  }
+  return resolve(kem->method_name);
+}
+
+OQS_STATUS OQS_KEM_keypair(const OQS_KEM* kem, uint8_t* pk, uint8_t* sk) {
+  const AlgInfo* a = alg_of(kem);
+  return a ? single(*a, Op::KEYPAIR, pk, sk, nullptr, nullptr) : OQS_ERROR;
+}
+OQS_STATUS OQS_KEM_keypair_derand(const OQS_KEM* kem, uint8_t* pk, uint8_t* sk, const uint8_t* seed) {
+  const AlgInfo* a = alg_of(kem);
+  if (!a || !seed) return OQS_ERROR;
+  return single(*a, Op::KEYPAIR, pk, sk, seed, nullptr);
+}
+OQS_STATUS OQS_KEM_encaps(const OQS_KEM* kem, uint8_t* ct, uint8_t* ss, const uint8_t* pk) {
+  const AlgInfo* a = alg_of(kem);
+  return a ? single(*a, Op::ENCAPS, ct, ss, pk, nullptr) : OQS_ERROR;
+}
+OQS_STATUS OQS_KEM_encaps_derand(const OQS_KEM* kem, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                                 const uint8_t* seed) {
+  const AlgInfo* a = alg_of(kem);
+  if (!a || !seed) return OQS_ERROR;
+  return single(*a, Op::ENCAPS, ct, ss, pk, seed);
+}
+OQS_STATUS OQS_KEM_decaps(const OQS_KEM* kem, uint8_t* ss, const uint8_t* ct, const uint8_t* sk) {
+  const AlgInfo* a = alg_of(kem);
+  return a ? single(*a, Op::DECAPS, ss, nullptr, ct, sk) : OQS_ERROR;
+}
+void OQS_KEM_free(OQS_KEM* kem) { free(kem); }
+
+void OQS_MEM_cleanse(void* ptr, size_t len) {
+  if (!ptr) return;
+  volatile uint8_t* p = (volatile uint8_t*)ptr;
+  while (len--) *p++ = 0;
+}
+
+// ------------------------------------------------------------------ Part 2: batched API
+int qrk_ctx_create(qrk_ctx** out, int device) {
+  if (!out) return fail("null out");
+  *out = nullptr;
+  if (ensure_device(device)) return -1;
+  qrk_ctx* c = new qrk_ctx();
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+void qrk_ctx_destroy(qrk_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->scratch || ctx->dstage) {
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+  }
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->dstage) (void)hipFree(ctx->dstage);
+  if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+  delete ctx;
+}
+
+int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {
+  if (!ctx || chunk == 0) return fail("bad chunk");
+  ctx->chunk = (chunk + 63) & ~(size_t)63;
+  return 0;
+}
+
+size_t qrk_ctx_scratch_bytes(const qrk_ctx* ctx) { return ctx ? ctx->scratch_bytes : 0; }
+
+int qrk_kem_sizes(const char* alg, size_t out[6]) {
+  const AlgInfo* a = find_alg(alg);
+  if (!a) return fail(std::string("unsupported KEM: ") + (alg ? alg : "(null)"));
+  out[0] = a->pk, out[1] = a->sk, out[2] = a->ct, out[3] = a->ss, out[4] = a->kp_coins, out[5] = a->enc_coins;
+  return 0;
+}
+
+#define QRK_RESOLVE(ctx, alg)                \
+  if (!(ctx)) return fail("null context");   \
+  const AlgInfo* a = resolve(alg);           \
+  if (!a) return -1;                         \
+  std::lock_guard<std::mutex> lk((ctx)->mu);
+
+int qrk_kem_keypair_batch(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
+                          void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch(ctx, *a, Op::KEYPAIR, n, pk, sk, coins, nullptr, nullptr, (hipStream_t)stream);
+}
+int qrk_kem_encaps_batch(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                         const uint8_t* coins, int32_t* status, void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch(ctx, *a, Op::ENCAPS, n, ct, ss, pk, coins, status, (hipStream_t)stream);
+}
+int qrk_kem_decaps_batch(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
+                         void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, nullptr, (hipStream_t)stream);
+}
+int qrk_kem_keypair_batch_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* pk, uint8_t* sk,
+                               const uint8_t* coins) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch_host(ctx, *a, Op::KEYPAIR, n, pk, sk, coins, nullptr, nullptr);
+}
+int qrk_kem_encaps_batch_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                              const uint8_t* coins, int32_t* status) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch_host(ctx, *a, Op::ENCAPS, n, ct, ss, pk, coins, status);
+}
+int qrk_kem_decaps_batch_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ss, const uint8_t* ct,
+                              const uint8_t* sk) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch_host(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, nullptr);
+}
+
+int qrk_bench_coins(qrk_ctx* ctx, size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, void* stream) {
+  if (!ctx) return fail("null context");
+  if (ensure_device(ctx->device)) return -1;
+  hipError_t e = bench_coins(n, len, seed, first, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("bench_coins", e);
+}
+
+int qrk_tamper(qrk_ctx* ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t* ct, void* stream) {
+  if (!ctx) return fail("null context");
+  if (ensure_device(ctx->device)) return -1;
+  hipError_t e = tamper_ciphertexts(n, ctlen, seed, mode, ct, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("tamper", e);
+}
+
+const char* qrk_last_error(void) { return g_err.c_str(); }
+
+int qrk_device_count(void) {
+  int c = 0;
+  return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+}
+
+}  // extern "C"

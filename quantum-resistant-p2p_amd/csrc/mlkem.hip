@@ -1,0 +1,990 @@
+// ML-KEM-512/768/1024 (FIPS 203) batched KeyGen / Encaps / Decaps for gfx950.
+//
+// Replaces, for N handshakes at once, the liboqs calls the reference makes one
+// at a time: OQS_KEM_keypair / OQS_KEM_encaps / OQS_KEM_decaps
+// (quantum_resistant_p2p/vendor/oqs.py:318, :348, :372), reached from
+// MLKEMKeyExchange.generate_keypair / encapsulate / decapsulate
+// (quantum_resistant_p2p/crypto/key_exchange.py:125-186).
+//
+// Decomposition (DESIGN.md "Kernels"): every handshake is split into
+// independent Keccak instances, each run by one lane, and polynomial stages,
+// each run by a 16-lane group per handshake.
+//
+//   k_front_*  lane / handshake   H(ek), G(.), J(z||c)             (SHA3 / SHAKE256)
+//   k_prf      lane / (nonce, hs)  PRF_eta(seed, N) raw bytes      (SHAKE256)
+//   k_xof      lane / (x, y, hs)   SampleNTT raw XOF blocks        (SHAKE128, 3-4 blocks)
+//   k_keygen_core / k_encrypt_core / k_decrypt_core
+//              16 lanes / hs       CBD, rejection compaction, NTT, basemul, invNTT,
+//                                  compress/encode, FO re-encrypt compare + implicit rejection
+//
+// Raw Keccak output goes to device scratch in a 64-instance tiled SoA layout
+// (word w of instance i at ((i/64)*W + w)*64 + i%64): every lane-per-instance
+// store is a fully coalesced 512-byte wave store.
+#include "keccak.cuh"
+#include "qrkem_internal.h"
+
+namespace qrk {
+namespace mlkem {
+
+constexpr int Q = 3329;
+constexpr int QINV = 62209;  // q^-1 mod 2^16
+constexpr int XOF_W = 84;    // four SHAKE128 blocks (168 B) of raw XOF output
+constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
+constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
+constexpr int R2 = 1353;       // R^2 mod q            (to Montgomery form)
+
+// ---------------------------------------------------------------- tables
+constexpr int powq(int b, int e) {
+  long r = 1;
+  for (int i = 0; i < e; ++i) r = (r * b) % Q;
+  return (int)r;
+}
+constexpr int br7(int i) {
+  int r = 0;
+  for (int b = 0; b < 7; ++b) r |= ((i >> b) & 1) << (6 - b);
+  return r;
+}
+constexpr int centered(long x) {
+  x %= Q;
+  if (x < 0) x += Q;
+  return (int)(x > Q / 2 ? x - Q : x);
+}
+struct Tables {
+  int zm[128];  // zeta_i * R mod q (centered): Montgomery-form NTT twiddles
+  int gm[128];  // gamma_i * R mod q: basemul moduli X^2 - gamma_i
+};
+constexpr Tables make_tables() {
+  Tables t{};
+  for (int i = 0; i < 128; ++i) {
+    t.zm[i] = centered((long)powq(17, br7(i)) * 65536);
+    t.gm[i] = centered((long)powq(17, 2 * br7(i) + 1) * 65536);
+  }
+  return t;
+}
+constexpr Tables TABC = make_tables();          // compile-time indexed twiddles
+__constant__ Tables TABD = make_tables();       // lane-indexed twiddles
+
+// ---------------------------------------------------------------- arithmetic
+// Signed Montgomery reduction, R = 2^16: returns a * R^-1 mod q, |r| < 2^15 + q/2.
+// 4 full-rate VALU ops: v_mul_u32_u24, v_bfe_i32, v_mad_i32_i24, v_ashrrev.
+__device__ __forceinline__ int mont_reduce(int a) {
+  const int t = (int)(int16_t)(uint16_t)__umul24((uint32_t)a, (uint32_t)QINV);
+  return (a - __mul24(t, Q)) >> 16;
+}
+__device__ __forceinline__ int fqmul(int a, int zm) { return mont_reduce(__mul24(a, zm)); }
+// Barrett to roughly [-q/2, q/2] for |a| < 2^17
+__device__ __forceinline__ int barrett(int a) {
+  const int t = (__mul24(a, 20159) + (1 << 25)) >> 26;
+  return a - __mul24(t, Q);
+}
+__device__ __forceinline__ int canon(int a) {
+  const int r = barrett(a);
+  return r + ((r >> 31) & Q);
+}
+// Compress_d(x) = round(2^d x / q) mod 2^d for x in [0, q): exact via 24-bit mulhi
+template <int D>
+__device__ __forceinline__ int compress(int x) {
+  const uint32_t y = ((uint32_t)x << D) + (Q / 2);
+  return (int)(__umulhi(y, 1290168u) & ((1u << D) - 1));
+}
+template <int D>
+__device__ __forceinline__ int decompress(int y) {
+  return (int)(((uint32_t)Q * (uint32_t)y + (1u << (D - 1))) >> D);
+}
+
+__device__ __forceinline__ size_t tidx(size_t inst, int w, int W) {
+  return ((inst >> 6) * (size_t)W + (size_t)w) * 64 + (inst & 63);
+}
+
+// 16-lane group synchronisation: a group never spans two waves, so ordering
+// LDS traffic inside the wave is enough.
+__device__ __forceinline__ void gsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// 8 consecutive 12-bit fields of the little-endian 96-bit string w0|w1|w2
+__device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, int c[8]) {
+  c[0] = (int)(w0 & 0xFFF);
+  c[1] = (int)((w0 >> 12) & 0xFFF);
+  c[2] = (int)(__builtin_amdgcn_alignbit(w1, w0, 24) & 0xFFF);
+  c[3] = (int)((w1 >> 4) & 0xFFF);
+  c[4] = (int)((w1 >> 16) & 0xFFF);
+  c[5] = (int)(__builtin_amdgcn_alignbit(w2, w1, 28) & 0xFFF);
+  c[6] = (int)((w2 >> 8) & 0xFFF);
+  c[7] = (int)(w2 >> 20);
+}
+
+__device__ __forceinline__ int count_lt_q(uint32_t w0, uint32_t w1, uint32_t w2) {
+  int c[8];
+  split12(w0, w1, w2, c);
+  int n = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) n += c[e] < Q;
+  return n;
+}
+
+// ============================================================ lane-per-instance Keccak kernels
+
+// SampleNTT producer: SHAKE128(rho || x || y), 3 squeezed blocks (+ a 4th when
+// the first 504 bytes hold fewer than 256 values < q), raw words to scratch.
+// inst = (x*K + y) * C + hs.
+template <int K>
+__global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
+                                             size_t n, size_t C, uint64_t* __restrict__ xof) {
+  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (inst >= (size_t)K * K * C) return;
+  const size_t hs = inst % C;
+  const int xy = (int)(inst / C);
+  if (hs >= n) return;
+  const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
+  KState s;
+  kzero(s);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
+  s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
+  s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
+  int cnt = 0;
+#pragma unroll 1
+  for (int b = 0; b < 4; ++b) {
+    if (b == 3 && cnt >= 256) break;
+    keccak_f(s);
+#pragma unroll
+    for (int w = 0; w < RW_SHAKE128; ++w) xof[tidx(inst, b * RW_SHAKE128 + w, XOF_W)] = kword(s, w);
+    if (b < 3) {
+      // 42 dwords = 14 triplets of 8 candidates
+#pragma unroll
+      for (int t = 0; t < 14; ++t) {
+        uint32_t d[3];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const int di = 3 * t + e;
+          d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
+        }
+        cnt += count_lt_q(d[0], d[1], d[2]);
+      }
+    }
+  }
+}
+
+// PRF producer: SHAKE256(seed || N) -> 64*eta bytes; inst = N * C + hs.
+// eta = (N < eta1_upto) ? ETA1 : ETA2.
+template <int ETA1, int ETA2>
+__global__ __launch_bounds__(256) void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
+                                             int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
+  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (inst >= (size_t)nprf * C) return;
+  const size_t hs = inst % C;
+  const int N = (int)(inst / C);
+  if (hs >= n) return;
+  const int eta = N < eta1_upto ? ETA1 : ETA2;
+  KState s;
+  kzero(s);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kxor(s, w, seeds[hs * 4 + w]);
+  s.a[4].lo ^= (uint32_t)N | (DS_SHAKE << 8);
+  s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  if (eta == 2) {
+#pragma unroll
+    for (int w = 0; w < 16; ++w) prf[tidx(inst, w, PRF_W)] = kword(s, w);
+  } else {
+#pragma unroll
+    for (int w = 0; w < 17; ++w) prf[tidx(inst, w, PRF_W)] = kword(s, w);
+    keccak_f(s);
+#pragma unroll
+    for (int w = 0; w < 7; ++w) prf[tidx(inst, 17 + w, PRF_W)] = kword(s, w);
+  }
+}
+
+template <int K>
+struct P {
+  static constexpr int ETA1 = (K == 2) ? 3 : 2;
+  static constexpr int ETA2 = 2;
+  static constexpr int DU = (K == 4) ? 11 : 10;
+  static constexpr int DV = (K == 4) ? 5 : 4;
+  static constexpr int PK = 384 * K + 32;
+  static constexpr int SK = 768 * K + 96;
+  static constexpr int CT = 32 * (DU * K + DV);
+};
+
+// KeyGen front: (rho, sigma) = G(d || k).  rho -> pk[384k..] and dk's ek copy; sigma -> seeds.
+template <int K>
+__global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict__ coins, size_t n,
+                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                      uint64_t* __restrict__ seeds) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+  KState s;
+  kzero(s);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kxor(s, w, d[w]);
+  s.a[4].lo ^= (uint32_t)K | (DS_SHA3 << 8);
+  s.a[RW_SHA3_512 - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  uint64_t* rho_pk = (uint64_t*)(pk + hs * P<K>::PK + 384 * K);
+  uint64_t* rho_sk = (uint64_t*)(sk + hs * P<K>::SK + 768 * K);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    rho_pk[w] = kword(s, w);
+    rho_sk[w] = kword(s, w);
+    seeds[hs * 4 + w] = kword(s, 4 + w);
+  }
+}
+
+// KeyGen back: dk = dk_pke || ek || H(ek) || z  (ek already copied by the core kernel)
+template <int K>
+__global__ __launch_bounds__(256) void k_back_keygen(const uint8_t* __restrict__ coins, size_t n,
+                                                     const uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
+  KState s;
+  kzero(s);
+  absorb_words<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, [&](int w) { return ek[w]; });
+  uint64_t* tail = (uint64_t*)(sk + hs * P<K>::SK + 768 * K + 32);
+  const uint64_t* z = (const uint64_t*)(coins + hs * 64 + 32);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    tail[w] = kword(s, w);
+    tail[4 + w] = z[w];
+  }
+}
+
+// Encaps front: (K, r) = G(m || H(ek)); K -> ss, r -> seeds
+template <int K>
+__global__ __launch_bounds__(256) void k_front_encaps(const uint8_t* __restrict__ pk,
+                                                      const uint8_t* __restrict__ coins, size_t n,
+                                                      uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
+  KState s;
+  kzero(s);
+  absorb_words<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, [&](int w) { return ek[w]; });
+  uint64_t h[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) h[w] = kword(s, w);
+  const uint64_t* m = (const uint64_t*)(coins + hs * 32);
+  kzero(s);
+  absorb_words<RW_SHA3_512, 8, DS_SHA3>(s, [&](int w) { return w < 4 ? m[w] : h[w - 4]; });
+  uint64_t* K_out = (uint64_t*)(ss + hs * 32);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    K_out[w] = kword(s, w);
+    seeds[hs * 4 + w] = kword(s, 4 + w);
+  }
+}
+
+// Decaps front: (K', r') = G(m' || h), Kbar = J(z || c)
+template <int K>
+__global__ __launch_bounds__(256) void k_front_decaps(const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk,
+                                                      const uint64_t* __restrict__ mprime, size_t n,
+                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
+                                                      uint64_t* __restrict__ kbar) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint64_t* h = (const uint64_t*)(sk + hs * P<K>::SK + 768 * K + 32);
+  const uint64_t* z = h + 4;
+  const uint64_t* m = mprime + hs * 4;
+  KState s;
+  kzero(s);
+  absorb_words<RW_SHA3_512, 8, DS_SHA3>(s, [&](int w) { return w < 4 ? m[w] : h[w - 4]; });
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    kprime[hs * 4 + w] = kword(s, w);
+    seeds[hs * 4 + w] = kword(s, 4 + w);
+  }
+  const uint64_t* c = (const uint64_t*)(ct + hs * P<K>::CT);
+  kzero(s);
+  absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
+}
+
+// ============================================================ 16-lane polynomial groups
+
+struct P16 {
+  int v[16];
+};
+
+// Per-group LDS: a padded 272-dword polynomial image (index j -> j + j/16, so both
+// the stride image [L + 16m] and the contiguous image [16L + t] are conflict-free)
+// plus 84 words of byte staging (raw XOF blocks, bit-packed encodings).
+constexpr int PBUF = 272;
+constexpr int RAWW = 84;
+struct GroupLds {
+  int poly[PBUF];
+  uint64_t raw[RAWW];
+};
+constexpr int GROUPS = 16;  // 256 threads
+
+__device__ __forceinline__ void stride_to_contig(P16& p, int* buf, int L) {
+#pragma unroll
+  for (int m = 0; m < 16; ++m) buf[L + 17 * m] = p.v[m];
+  gsync();
+#pragma unroll
+  for (int t = 0; t < 16; ++t) p.v[t] = buf[17 * L + t];
+  gsync();
+}
+__device__ __forceinline__ void contig_to_stride(P16& p, int* buf, int L) {
+#pragma unroll
+  for (int t = 0; t < 16; ++t) buf[17 * L + t] = p.v[t];
+  gsync();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) p.v[m] = buf[L + 17 * m];
+  gsync();
+}
+
+// FIPS 203 Alg. 9.  In: stride layout (v[m] = f[L+16m]).  Out: contiguous (v[t] = f[16L+t]).
+__device__ __forceinline__ void ntt_fwd(P16& p, int* buf, int L) {
+#pragma unroll
+  for (int lg = 0; lg < 4; ++lg) {
+    const int step = 8 >> lg;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (((m / step) & 1) == 0) {
+        const int zeta = TABC.zm[(1 << lg) + m / (2 * step)];
+        const int t = fqmul(p.v[m + step], zeta);
+        p.v[m + step] = p.v[m] - t;
+        p.v[m] = p.v[m] + t;
+      }
+    }
+  }
+  stride_to_contig(p, buf, L);
+  {
+    const int z = TABD.zm[16 + L];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int u = fqmul(p.v[t + 8], z);
+      p.v[t + 8] = p.v[t] - u;
+      p.v[t] = p.v[t] + u;
+    }
+  }
+  {
+    const int z0 = TABD.zm[32 + 2 * L], z1 = TABD.zm[33 + 2 * L];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 2) & 1) == 0) {
+        const int u = fqmul(p.v[t + 4], t < 8 ? z0 : z1);
+        p.v[t + 4] = p.v[t] - u;
+        p.v[t] = p.v[t] + u;
+      }
+    }
+  }
+  {
+    int z[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z[s] = TABD.zm[64 + 4 * L + s];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 1) & 1) == 0) {
+        const int u = fqmul(p.v[t + 2], z[t >> 2]);
+        p.v[t + 2] = p.v[t] - u;
+        p.v[t] = p.v[t] + u;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) p.v[t] = barrett(p.v[t]);
+}
+
+// FIPS 203 Alg. 10 (times R, see F_SCALE).  In: contiguous.  Out: stride layout.
+__device__ __forceinline__ void ntt_inv(P16& p, int* buf, int L) {
+  {
+    int z[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z[s] = TABD.zm[127 - 4 * L - s];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 1) & 1) == 0) {
+        const int x = p.v[t], y = p.v[t + 2];
+        p.v[t] = x + y;
+        p.v[t + 2] = fqmul(y - x, z[t >> 2]);
+      }
+    }
+  }
+  {
+    const int z0 = TABD.zm[63 - 2 * L], z1 = TABD.zm[62 - 2 * L];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 2) & 1) == 0) {
+        const int x = p.v[t], y = p.v[t + 4];
+        p.v[t] = x + y;
+        p.v[t + 4] = fqmul(y - x, t < 8 ? z0 : z1);
+      }
+    }
+  }
+  {
+    const int z = TABD.zm[31 - L];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int x = p.v[t], y = p.v[t + 8];
+      p.v[t] = x + y;
+      p.v[t + 8] = fqmul(y - x, z);
+    }
+  }
+  contig_to_stride(p, buf, L);
+#pragma unroll
+  for (int lg = 3; lg >= 0; --lg) {
+    const int step = 8 >> lg;  // len/16 for len = 16 << (3 - lg)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (((m / step) & 1) == 0) {
+        const int zeta = TABC.zm[(2 << lg) - 1 - m / (2 * step)];
+        const int x = p.v[m], y = p.v[m + step];
+        p.v[m] = x + y;
+        p.v[m + step] = fqmul(y - x, zeta);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) p.v[m] = fqmul(p.v[m], F_SCALE);
+}
+
+// b1*gamma for the 8 coefficient pairs of a contiguous NTT-domain operand
+__device__ __forceinline__ void pair_gamma(const P16& b, int g[8], int L) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) g[u] = fqmul(b.v[2 * u + 1], TABD.gm[8 * L + u]);
+}
+
+// acc += a o b   (a in [0,q), b and bg centered): 4 mad24 per pair, reduced later
+__device__ __forceinline__ void basemul_acc(int acc[16], const P16& a, const P16& b, const int bg[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int a0 = a.v[2 * u], a1 = a.v[2 * u + 1];
+    acc[2 * u] += __mul24(a0, b.v[2 * u]) + __mul24(a1, bg[u]);
+    acc[2 * u + 1] += __mul24(a0, b.v[2 * u + 1]) + __mul24(a1, b.v[2 * u]);
+  }
+}
+
+// CBD_eta from the PRF instance's raw words; contiguous layout.
+template <int ETA>
+__device__ __forceinline__ void cbd(P16& p, const uint64_t* __restrict__ prf, size_t inst, int L) {
+  if constexpr (ETA == 2) {
+    const uint64_t w = prf[tidx(inst, L, PRF_W)];
+    const uint32_t d[2] = {(uint32_t)w, (uint32_t)(w >> 32)};
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t f = (d[t >> 3] >> (4 * (t & 7))) & 0xF;
+      p.v[t] = (int)__popc(f & 3u) - (int)__popc(f & 0xCu);
+    }
+  } else {
+    const int wi = (3 * L) >> 1;
+    const uint64_t a = prf[tidx(inst, wi, PRF_W)], b = prf[tidx(inst, wi + 1, PRF_W)];
+    const bool odd = L & 1;
+    const uint32_t d0 = odd ? (uint32_t)(a >> 32) : (uint32_t)a;
+    const uint32_t d1 = odd ? (uint32_t)b : (uint32_t)(a >> 32);
+    const uint32_t d[3] = {d0, d1, odd ? (uint32_t)(b >> 32) : (uint32_t)b};
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int bit = 6 * t, i = bit >> 5, sh = bit & 31;
+      uint32_t f = d[i] >> sh;
+      if (sh + 6 > 32) f |= d[i + 1] << (32 - sh);
+      f &= 0x3F;
+      p.v[t] = (int)__popc(f & 7u) - (int)__popc(f & 0x38u);
+    }
+  }
+}
+
+// Group-cooperative load of 16*D*2 bytes at src (4-byte aligned) into the raw
+// stage, then lane L unpacks its 16 D-bit fields (bits 16*D*L ...).
+template <int D>
+__device__ __forceinline__ void load_bits(P16& p, const uint8_t* __restrict__ src, GroupLds& g, int L) {
+  constexpr int NDW = 8 * D;  // dwords for 256 D-bit values
+  uint32_t* st = (uint32_t*)g.raw;
+  const uint32_t* s32 = (const uint32_t*)src;
+#pragma unroll
+  for (int i = 0; i < (NDW + 15) / 16; ++i) {
+    const int idx = L + 16 * i;
+    if (idx < NDW) st[idx] = s32[idx];
+  }
+  gsync();
+  // this lane's 2D bytes start at byte 2*D*L
+  const int b0 = 2 * D * L;
+  uint32_t w[8];
+  const uint16_t* st16 = (const uint16_t*)g.raw;
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    // assemble dwords from halfwords (2D bytes = D halfwords)
+    const uint32_t h = st16[(b0 >> 1) + j];
+    if (j & 1)
+      w[j >> 1] |= h << 16;
+    else
+      w[j >> 1] = h;
+  }
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int bit = D * t;
+    const int i = bit >> 5, sh = bit & 31;
+    uint32_t v = w[i] >> sh;
+    if (sh + D > 32) v |= w[i + 1] << (32 - sh);
+    p.v[t] = (int)(v & ((1u << D) - 1));
+  }
+  gsync();
+}
+
+// Pack lane L's 16 D-bit fields into the raw stage at byte 2*D*L (whole group: 32*D bytes).
+template <int D>
+__device__ __forceinline__ void pack_bits(const P16& p, GroupLds& g, int L) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = 0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int bit = D * t;
+    const int i = bit >> 5, sh = bit & 31;
+    const uint32_t v = (uint32_t)p.v[t];
+    w[i] |= v << sh;
+    if (sh + D > 32) w[i + 1] |= v >> (32 - sh);
+  }
+  uint16_t* st16 = (uint16_t*)g.raw;
+  const int h0 = D * L;
+#pragma unroll
+  for (int j = 0; j < D; ++j) st16[h0 + j] = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+  gsync();
+}
+
+// Store the packed stage (8*D dwords) to dst; or, when cmp != nullptr, OR the
+// XOR with cmp into diff instead (Decaps re-encryption compare).
+template <int D>
+__device__ __forceinline__ void flush_bits(GroupLds& g, uint8_t* dst, const uint8_t* cmp, uint32_t& diff,
+                                           bool active, int L) {
+  constexpr int NDW = 8 * D;
+  const uint32_t* st = (const uint32_t*)g.raw;
+#pragma unroll
+  for (int i = 0; i < (NDW + 15) / 16; ++i) {
+    const int idx = L + 16 * i;
+    if (idx < NDW) {
+      const uint32_t v = st[idx];
+      if (cmp)
+        diff |= v ^ ((const uint32_t*)cmp)[idx];
+      else if (active)
+        ((uint32_t*)dst)[idx] = v;
+    }
+  }
+  gsync();
+}
+
+// SampleNTT consumer: copy the raw XOF words of `inst` to LDS, compact values < q
+// in stream order (group prefix sums), return the polynomial in contiguous layout.
+__device__ __forceinline__ void sample_ntt(P16& a, const uint64_t* __restrict__ xof, size_t inst, GroupLds& g,
+                                           int L) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int w = L + 16 * i;
+    if (w < 63) g.raw[w] = xof[tidx(inst, w, XOF_W)];
+  }
+  gsync();
+  const uint32_t* r32 = (const uint32_t*)g.raw;
+  int total = 0;
+#pragma unroll 1
+  for (int blk = 0; blk < 4; ++blk) {
+    if (blk == 3) {
+      if (total >= 256) break;
+      // rare: fourth block (producer squeezed it for exactly this case)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int w = 63 + L + 16 * i;
+        if (w < 84) g.raw[w] = xof[tidx(inst, w, XOF_W)];
+      }
+      gsync();
+    }
+    int c[8];
+    const bool lane_ok = L < 14;
+    const int d0 = 42 * blk + 3 * L;
+    if (lane_ok) {
+      split12(r32[d0], r32[d0 + 1], r32[d0 + 2], c);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c[e] = Q;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cnt += c[e] < Q;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const int o = __shfl_up(incl, d, 16);
+      if (L >= d) incl += o;
+    }
+    int pos = total + incl - cnt;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (c[e] < Q) {
+        if (pos < 256) g.poly[pos + (pos >> 4)] = c[e];
+        ++pos;
+      }
+    }
+    total += __shfl(incl, 15, 16);
+  }
+  gsync();
+#pragma unroll
+  for (int t = 0; t < 16; ++t) a.v[t] = g.poly[17 * L + t];
+  gsync();
+}
+
+// 12-bit decode of a 384-byte encoded NTT-domain polynomial; optional modulus check.
+__device__ __forceinline__ void decode12(P16& p, const uint8_t* __restrict__ src, bool& bad, int L) {
+  const uint64_t* s = (const uint64_t*)(src + 24 * L);
+  const uint64_t a = s[0], b = s[1], c = s[2];
+  int v[16];
+  split12((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, v);
+  split12((uint32_t)(b >> 32), (uint32_t)c, (uint32_t)(c >> 32), v + 8);
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    bad |= v[t] >= Q;
+    p.v[t] = v[t] >= Q ? v[t] - Q : v[t];
+  }
+}
+
+__device__ __forceinline__ void encode12(const P16& p, uint8_t* dst, int L) {
+  uint32_t w[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) w[i] = 0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int bit = 12 * t, i = bit >> 5, sh = bit & 31;
+    const uint32_t v = (uint32_t)p.v[t];
+    w[i] |= v << sh;
+    if (sh + 12 > 32) w[i + 1] |= v >> (32 - sh);
+  }
+  uint64_t* d = (uint64_t*)(dst + 24 * L);
+  d[0] = ((uint64_t)w[1] << 32) | w[0];
+  d[1] = ((uint64_t)w[3] << 32) | w[2];
+  d[2] = ((uint64_t)w[5] << 32) | w[4];
+}
+
+__device__ __forceinline__ uint32_t group_or(uint32_t x) {
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) x |= __shfl_xor(x, d, 16);
+  return x;
+}
+
+// Scratch carve-up for a chunk of C handshakes
+struct ScratchView {
+  uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
+};
+__host__ __device__ inline size_t scratch_words(int K, size_t C) {
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C;
+}
+inline ScratchView carve(void* base, int K, size_t C) {
+  ScratchView v;
+  uint64_t* p = (uint64_t*)base;
+  v.xof = p;
+  p += (size_t)K * K * C * XOF_W;
+  v.prf = p;
+  p += (size_t)(2 * K + 1) * C * PRF_W;
+  v.seeds = p;
+  p += 4 * C;
+  v.mprime = p;
+  p += 4 * C;
+  v.kprime = p;
+  p += 4 * C;
+  v.kbar = p;
+  return v;
+}
+
+// ------------------------------------------------------------ KeyGen core
+// s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
+// t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
+template <int K>
+__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+                                                     const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
+                                                     uint8_t* __restrict__ sk) {
+  __shared__ GroupLds lds[GROUPS];
+  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  GroupLds& g = lds[gi];
+  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
+  const bool active = hs_raw < n;
+  const size_t hs = active ? hs_raw : n - 1;
+  P16 sh[K];
+  int sg[K][8];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    P16 t;
+    cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
+    contig_to_stride(t, g.poly, L);
+    ntt_fwd(t, g.poly, L);
+    sh[j] = t;
+    pair_gamma(t, sg[j], L);
+  }
+  uint8_t* ek = pk + hs * P<K>::PK;
+  uint8_t* dk = sk + hs * P<K>::SK;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    P16 s;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) s.v[x] = canon(sh[j].v[x]);
+    if (active) encode12(s, dk + 384 * j, L);
+  }
+#pragma unroll 1
+  for (int i = 0; i < K; ++i) {
+    int acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P16 a;
+      sample_ntt(a, xof, (size_t)(j * K + i) * C + hs, g, L);
+      basemul_acc(acc, a, sh[j], sg[j]);
+    }
+    P16 e;
+    cbd<P<K>::ETA1>(e, prf, (size_t)(K + i) * C + hs, L);
+    contig_to_stride(e, g.poly, L);
+    ntt_fwd(e, g.poly, L);
+    P16 t;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) t.v[x] = canon(fqmul(mont_reduce(acc[x]), R2) + e.v[x]);
+    if (active) {
+      encode12(t, ek + 384 * i, L);
+      encode12(t, dk + 384 * K + 384 * i, L);
+    }
+  }
+}
+
+// ------------------------------------------------------------ K-PKE.Encrypt core
+// MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
+// select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+                                                      const uint64_t* __restrict__ prf,
+                                                      const uint8_t* __restrict__ ek_base, size_t ek_stride,
+                                                      const uint8_t* __restrict__ m_base, size_t m_stride,
+                                                      uint8_t* __restrict__ ct, int32_t* __restrict__ status,
+                                                      const uint64_t* __restrict__ kprime,
+                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
+  constexpr int DU = P<K>::DU, DV = P<K>::DV;
+  __shared__ GroupLds lds[GROUPS];
+  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  GroupLds& g = lds[gi];
+  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
+  const bool active = hs_raw < n;
+  const size_t hs = active ? hs_raw : n - 1;
+  const uint8_t* ek = ek_base + hs * ek_stride;
+  uint8_t* c = ct + hs * P<K>::CT;
+  uint32_t diff = 0;
+
+  P16 yh[K];
+  int yg[K][8];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    P16 t;
+    cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
+    contig_to_stride(t, g.poly, L);
+    ntt_fwd(t, g.poly, L);
+    yh[j] = t;
+    pair_gamma(t, yg[j], L);
+  }
+  // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j)
+#pragma unroll 1
+  for (int i = 0; i < K; ++i) {
+    int acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P16 a;
+      sample_ntt(a, xof, (size_t)(i * K + j) * C + hs, g, L);
+      basemul_acc(acc, a, yh[j], yg[j]);
+    }
+    P16 u;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) u.v[t] = mont_reduce(acc[t]);
+    ntt_inv(u, g.poly, L);
+    stride_to_contig(u, g.poly, L);
+    P16 e;
+    cbd<P<K>::ETA2>(e, prf, (size_t)(K + i) * C + hs, L);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon(u.v[t] + e.v[t]));
+    pack_bits<DU>(u, g, L);
+    flush_bits<DU>(g, c + 32 * DU * i, MODE ? c + 32 * DU * i : nullptr, diff, active, L);
+  }
+  // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
+  {
+    int acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      P16 th;
+      decode12(th, ek + 384 * j, bad, L);
+      basemul_acc(acc, th, yh[j], yg[j]);
+    }
+    P16 v;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) v.v[t] = mont_reduce(acc[t]);
+    ntt_inv(v, g.poly, L);
+    stride_to_contig(v, g.poly, L);
+    P16 e;
+    cbd<P<K>::ETA2>(e, prf, (size_t)(2 * K) * C + hs, L);
+    const uint8_t* m = m_base + hs * m_stride;
+    const uint32_t mb = (uint32_t)m[2 * L] | ((uint32_t)m[2 * L + 1] << 8);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int mu = ((mb >> t) & 1) ? (Q + 1) / 2 : 0;
+      v.v[t] = compress<DV>(canon(v.v[t] + e.v[t] + mu));
+    }
+    pack_bits<DV>(v, g, L);
+    flush_bits<DV>(g, c + 32 * DU * K, MODE ? c + 32 * DU * K : nullptr, diff, active, L);
+    if (MODE == 0 && status) {
+      const uint32_t anybad = group_or(bad ? 1u : 0u);
+      if (active && L == 0) status[hs] = anybad ? -1 : 0;
+    }
+  }
+  if (MODE == 1) {
+    // constant-time select: ss = (c == c') ? K' : Kbar
+    const uint32_t d = group_or(diff);
+    const uint32_t mask = (uint32_t)(((uint64_t)d - 1u) >> 32);  // all-ones iff d == 0, no branch
+    if (L < 8) {
+      const uint32_t kp = ((const uint32_t*)(kprime + hs * 4))[L];
+      const uint32_t kb = ((const uint32_t*)(kbar + hs * 4))[L];
+      if (active) ((uint32_t*)(ss + hs * 32))[L] = (kp & mask) | (kb & ~mask);
+    }
+  }
+}
+
+// ------------------------------------------------------------ K-PKE.Decrypt core
+template <int K>
+__global__ __launch_bounds__(256) void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
+  constexpr int DU = P<K>::DU, DV = P<K>::DV;
+  __shared__ GroupLds lds[GROUPS];
+  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  GroupLds& g = lds[gi];
+  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
+  const bool active = hs_raw < n;
+  const size_t hs = active ? hs_raw : n - 1;
+  const uint8_t* c = ct + hs * P<K>::CT;
+  const uint8_t* dk = sk + hs * P<K>::SK;
+  int acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = 0;
+  bool bad = false;
+#pragma unroll 1
+  for (int j = 0; j < K; ++j) {
+    P16 u;
+    load_bits<DU>(u, c + 32 * DU * j, g, L);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) u.v[t] = decompress<DU>(u.v[t]);
+    contig_to_stride(u, g.poly, L);
+    ntt_fwd(u, g.poly, L);
+    int ug[8];
+    pair_gamma(u, ug, L);
+    P16 s;
+    decode12(s, dk + 384 * j, bad, L);
+    basemul_acc(acc, s, u, ug);
+  }
+  P16 w;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) w.v[t] = mont_reduce(acc[t]);
+  ntt_inv(w, g.poly, L);
+  stride_to_contig(w, g.poly, L);
+  P16 v;
+  load_bits<DV>(v, c + 32 * DU * K, g, L);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int x = canon(decompress<DV>(v.v[t]) - w.v[t]);
+    bits |= (uint32_t)compress<1>(x) << t;
+  }
+  if (active) ((uint16_t*)(mprime + hs * 4))[L] = (uint16_t)bits;
+}
+
+// ============================================================ host launchers
+
+inline unsigned blocks_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
+inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+template <int K>
+hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
+  const size_t C = round64(n);
+  ScratchView v = carve(scratch, K, C);
+  hipLaunchKernelGGL(k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk, v.seeds);
+  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds, n,
+                     C, 2 * K, 2 * K, v.prf);
+  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
+                     (size_t)P<K>::PK, n, C, v.xof);
+  hipLaunchKernelGGL(k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C, v.xof,
+                     v.prf, pk, sk);
+  hipLaunchKernelGGL(k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
+                       int32_t* status, void* scratch, hipStream_t st) {
+  const size_t C = round64(n);
+  ScratchView v = carve(scratch, K, C);
+  hipLaunchKernelGGL(k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss, v.seeds);
+  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+                     v.seeds, n, C, 2 * K + 1, K, v.prf);
+  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
+                     (size_t)P<K>::PK, n, C, v.xof);
+  hipLaunchKernelGGL((k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C,
+                     v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch, hipStream_t st) {
+  const size_t C = round64(n);
+  ScratchView v = carve(scratch, K, C);
+  const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
+  hipLaunchKernelGGL(k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
+  hipLaunchKernelGGL(k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n, v.seeds,
+                     v.kprime, v.kbar);
+  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+                     v.seeds, n, C, 2 * K + 1, K, v.prf);
+  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, sk + 768 * K,
+                     (size_t)P<K>::SK, n, C, v.xof);
+  hipLaunchKernelGGL((k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf, sk + 384 * K,
+                     (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
+                     (int32_t*)nullptr, v.kprime, v.kbar, ss);
+  return hipGetLastError();
+}
+
+}  // namespace mlkem
+
+size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
+  return mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8;
+}
+
+hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
+                         hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 2: return mlkem::keygen_impl<2>(n, pk, sk, coins, scratch, st);
+    case 3: return mlkem::keygen_impl<3>(n, pk, sk, coins, scratch, st);
+    case 4: return mlkem::keygen_impl<4>(n, pk, sk, coins, scratch, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t mlkem_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                        const uint8_t* coins, int32_t* status, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 2: return mlkem::encaps_impl<2>(n, ct, ss, pk, coins, status, scratch, st);
+    case 3: return mlkem::encaps_impl<3>(n, ct, ss, pk, coins, status, scratch, st);
+    case 4: return mlkem::encaps_impl<4>(n, ct, ss, pk, coins, status, scratch, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t mlkem_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
+                        void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 2: return mlkem::decaps_impl<2>(n, ss, ct, sk, scratch, st);
+    case 3: return mlkem::decaps_impl<3>(n, ss, ct, sk, scratch, st);
+    case 4: return mlkem::decaps_impl<4>(n, ss, ct, sk, scratch, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace qrk

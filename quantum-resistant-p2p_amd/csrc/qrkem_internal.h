@@ -1,0 +1,60 @@
+// Internal host-side interface between the C-ABI (abi.cpp) and the kernel
+// launchers (mlkem.hip, frodo.hip, util.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace qrk {
+
+enum class Family { MLKEM, FRODO };
+
+struct AlgInfo {
+  const char* name;
+  Family family;
+  int level;        // claimed NIST level (OQS_KEM.claimed_nist_level)
+  int k;            // ML-KEM module rank, or Frodo n
+  size_t pk, sk, ct, ss;
+  size_t kp_coins, enc_coins;  // bytes drawn by one keypair / encaps randombytes call
+  bool aes;         // Frodo A generated with AES-128 (else SHAKE128)
+  bool enabled;     // has a HIP implementation in this build
+};
+
+const AlgInfo* find_alg(const char* name);
+int alg_count();
+const AlgInfo* alg_at(int i);
+
+// Device scratch owned by a context.  Grown on demand, never shrunk.
+struct Scratch {
+  void* base = nullptr;
+  size_t bytes = 0;
+};
+
+// Per-chunk scratch requirement (bytes) for `chunk` handshakes of `a`.
+size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk);
+size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk);
+
+// All pointers are device pointers; n handshakes processed as one chunk
+// (the caller splits large batches).  Return hipError_t.
+hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
+                         void* scratch, hipStream_t st);
+hipError_t mlkem_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                        const uint8_t* coins, int32_t* status, void* scratch, hipStream_t st);
+hipError_t mlkem_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
+                        void* scratch, hipStream_t st);
+
+hipError_t frodo_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
+                         void* scratch, hipStream_t st);
+hipError_t frodo_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
+                        const uint8_t* coins, void* scratch, hipStream_t st);
+hipError_t frodo_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
+                        void* scratch, hipStream_t st);
+
+// SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len) for i < n, len <= 136.
+hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st);
+
+// Flip one bit of ct_i for the indices selected by SHAKE256-derived Bernoulli(1/2)
+// (bench config 5).  mode: 0 none, 1 all, 2 mixed.
+hipError_t tamper_ciphertexts(size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t* ct, hipStream_t st);
+
+}  // namespace qrk

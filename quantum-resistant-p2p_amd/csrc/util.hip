@@ -1,0 +1,87 @@
+// Bench-input helpers that run on the device so that 2^20..2^24-handshake
+// inputs never cross PCIe.
+#include "keccak.cuh"
+#include "qrkem_internal.h"
+
+namespace qrk {
+
+// coins_i = SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len), len <= 136
+__global__ __launch_bounds__(256) void k_bench_coins(size_t n, int nwords, uint64_t seed, uint64_t first,
+                                                     uint64_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t idx = first + i;
+  // 25-byte message: "qrk-benc" | "h" seed[0..6] | seed[7] idx[0..6] | idx[7] DS
+  const uint64_t w0 = 0x636e65622d6b7271ull;  // "qrk-benc" little-endian
+  const uint64_t w1 = 0x68ull | (seed << 8);
+  const uint64_t w2 = (seed >> 56) | (idx << 8);
+  const uint64_t w3 = (idx >> 56) | ((uint64_t)DS_SHAKE << 8);
+  KState s;
+  kzero(s);
+  kxor(s, 0, w0);
+  kxor(s, 1, w1);
+  kxor(s, 2, w2);
+  kxor(s, 3, w3);
+  s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  uint64_t* o = out + i * (size_t)nwords;
+#pragma unroll
+  for (int w = 0; w < RW_SHAKE256; ++w)
+    if (w < nwords) o[w] = kword(s, w);
+}
+
+hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st) {
+  if (len % 8 || len > 136) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bench_coins, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, (int)(len / 8), seed,
+                     first, (uint64_t*)out);
+  return hipGetLastError();
+}
+
+// h_i = SHAKE256("qrk-tamper" || LE64(seed) || LE64(i)) first 8 bytes;
+// tamper iff mode == 1, or mode == 2 and (h_i & 1); flipped bit = (h_i >> 1) mod (8 * ctlen)
+__global__ __launch_bounds__(256) void k_tamper(size_t n, size_t ctlen, uint64_t seed, int mode,
+                                                uint8_t* __restrict__ ct) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  // 26-byte message: "qrk-tamp" | "er" seed[0..5] | seed[6..7] i[0..5] | i[6..7] DS
+  const uint64_t idx = i;
+  KState s;
+  kzero(s);
+  kxor(s, 0, 0x706d61742d6b7271ull);  // "qrk-tamp"
+  kxor(s, 1, 0x7265ull | (seed << 16));
+  kxor(s, 2, (seed >> 48) | (idx << 16));
+  kxor(s, 3, (idx >> 48) | ((uint64_t)DS_SHAKE << 16));
+  s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  const uint64_t h = kword(s, 0);
+  const bool flip = mode == 1 || (mode == 2 && (h & 1));
+  if (flip) {
+    const uint64_t bit = (h >> 1) % (8 * ctlen);
+    ct[i * ctlen + bit / 8] ^= (uint8_t)(1u << (bit % 8));
+  }
+}
+
+hipError_t tamper_ciphertexts(size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t* ct, hipStream_t st) {
+  if (n == 0 || mode == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tamper, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, ctlen, seed, mode, ct);
+  return hipGetLastError();
+}
+
+// FrodoKEM: HIP implementation lands in frodo.hip; until then the algorithms are
+// listed as supported-but-not-enabled (OQS_KEM_alg_is_enabled == 0).
+__attribute__((weak)) size_t frodo_scratch_bytes(const AlgInfo&, size_t) { return 0; }
+__attribute__((weak)) hipError_t frodo_keypair(const AlgInfo&, size_t, uint8_t*, uint8_t*, const uint8_t*, void*,
+                                               hipStream_t) {
+  return hipErrorNotSupported;
+}
+__attribute__((weak)) hipError_t frodo_encaps(const AlgInfo&, size_t, uint8_t*, uint8_t*, const uint8_t*,
+                                              const uint8_t*, void*, hipStream_t) {
+  return hipErrorNotSupported;
+}
+__attribute__((weak)) hipError_t frodo_decaps(const AlgInfo&, size_t, uint8_t*, const uint8_t*, const uint8_t*,
+                                              void*, hipStream_t) {
+  return hipErrorNotSupported;
+}
+
+}  // namespace qrk

@@ -1,0 +1,174 @@
+"""Batched KEM engine: N independent handshakes per call on one MI355X.
+
+The reference performs one ``OQS_KEM_*`` call per handshake on the asyncio
+thread (``quantum_resistant_p2p/crypto/key_exchange.py:133,155-156,178-179``).
+:class:`BatchKEM` runs N of them per call through ``qrk_kem_*_batch`` in
+libqrkem.so.  Device tensors (``torch.uint8`` on ``cuda``) are passed by pointer
+and processed on the caller's current stream (zero copy); host arrays go through
+the synchronous ``*_batch_host`` entry points.
+
+Tensors are contiguous ``[n, len]`` uint8 -- the AoS layout the C ABI documents.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from typing import Optional
+
+import numpy as np
+
+from ._native import LIB, last_error
+from .oqs import MechanismNotEnabledError, MechanismNotSupportedError, get_enabled_kem_mechanisms, \
+    get_supported_kem_mechanisms, kem_sizes
+
+try:  # torch is plumbing for device memory/streams, not a compute path
+    import torch
+except ImportError:  # pragma: no cover
+    torch = None
+
+
+def _is_dev(x) -> bool:
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def _dptr(t) -> ct.c_void_p:
+    assert t.dtype == torch.uint8 or t.dtype == torch.int32, t.dtype
+    assert t.is_contiguous()
+    return ct.c_void_p(t.data_ptr())
+
+
+def _hptr(a: np.ndarray) -> ct.c_void_p:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(ct.c_void_p)
+
+
+def _as_host(x, width: int) -> np.ndarray:
+    if isinstance(x, (bytes, bytearray)):
+        x = np.frombuffer(bytes(x), np.uint8).reshape(1, -1)
+    elif isinstance(x, (list, tuple)):
+        x = np.stack([np.frombuffer(bytes(b), np.uint8) for b in x]) if x else np.zeros((0, width), np.uint8)
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.uint8))
+    if a.ndim != 2 or a.shape[1] != width:
+        raise ValueError(f"expected a [n, {width}] uint8 array, got shape {a.shape}")
+    return a
+
+
+class BatchKEM:
+    """Batched KeyGen / Encaps / Decaps for one algorithm on one device."""
+
+    def __init__(self, alg: str, device: int = 0, chunk: Optional[int] = None):
+        if alg not in get_enabled_kem_mechanisms():
+            if alg in get_supported_kem_mechanisms():
+                raise MechanismNotEnabledError(alg)
+            raise MechanismNotSupportedError(alg)
+        self.alg = alg
+        self._name = alg.encode()
+        self.device = device
+        s = kem_sizes(alg)
+        self.pk_len = s["length_public_key"]
+        self.sk_len = s["length_secret_key"]
+        self.ct_len = s["length_ciphertext"]
+        self.ss_len = s["length_shared_secret"]
+        self.kp_coins = s["length_keypair_coins"]
+        self.enc_coins = s["length_encaps_coins"]
+        h = ct.c_void_p()
+        if LIB.qrk_ctx_create(ct.byref(h), device) != 0:
+            raise RuntimeError(f"qrkem: cannot create a context on device {device}: {last_error()}")
+        self._ctx = h
+        if chunk:
+            LIB.qrk_ctx_set_chunk(self._ctx, chunk)
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            LIB.qrk_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ct.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise RuntimeError(f"qrkem {what} failed ({self.alg}): {last_error()}")
+
+    def _empty(self, n: int, width: int):
+        return torch.empty((n, width), dtype=torch.uint8, device=f"cuda:{self.device}")
+
+    # ------------------------------------------------------------------ KeyGen
+    def keypair(self, n: Optional[int] = None, coins=None):
+        """Returns (pk [n, pk_len], sk [n, sk_len]).  ``coins`` [n, kp_coins] or None (OS CSPRNG).
+
+        Device coins (or ``n`` without coins) -> device outputs; host coins -> numpy outputs."""
+        if coins is None and n is None:
+            raise ValueError("give n or coins")
+        if coins is not None and not _is_dev(coins):
+            c = _as_host(coins, self.kp_coins)
+            n = c.shape[0]
+            pk = np.zeros((n, self.pk_len), np.uint8)
+            sk = np.zeros((n, self.sk_len), np.uint8)
+            self._check(LIB.qrk_kem_keypair_batch_host(self._ctx, self._name, n, _hptr(pk), _hptr(sk), _hptr(c)),
+                        "keypair")
+            return pk, sk
+        n = coins.shape[0] if coins is not None else n
+        pk, sk = self._empty(n, self.pk_len), self._empty(n, self.sk_len)
+        cp = _dptr(coins) if coins is not None else None
+        self._check(LIB.qrk_kem_keypair_batch(self._ctx, self._name, n, _dptr(pk), _dptr(sk), cp, self._stream()),
+                    "keypair")
+        return pk, sk
+
+    # ------------------------------------------------------------------ Encaps
+    def encaps(self, pk, coins=None, return_status: bool = False):
+        """Returns (ct, ss) (+ status int32[n]: -1 where pk fails the FIPS 203 7.2 check)."""
+        if _is_dev(pk):
+            n = pk.shape[0]
+            c, ss = self._empty(n, self.ct_len), self._empty(n, self.ss_len)
+            st = torch.empty((n,), dtype=torch.int32, device=pk.device) if return_status else None
+            if coins is not None and not _is_dev(coins):
+                coins = torch.from_numpy(_as_host(coins, self.enc_coins)).to(pk.device)
+            self._check(LIB.qrk_kem_encaps_batch(self._ctx, self._name, n, _dptr(c), _dptr(ss), _dptr(pk),
+                                                 _dptr(coins) if coins is not None else None,
+                                                 _dptr(st) if st is not None else None, self._stream()), "encaps")
+            return (c, ss, st) if return_status else (c, ss)
+        p = _as_host(pk, self.pk_len)
+        n = p.shape[0]
+        c = np.zeros((n, self.ct_len), np.uint8)
+        ss = np.zeros((n, self.ss_len), np.uint8)
+        st = np.zeros((n,), np.int32)
+        cc = _as_host(coins, self.enc_coins) if coins is not None else None
+        self._check(LIB.qrk_kem_encaps_batch_host(self._ctx, self._name, n, _hptr(c), _hptr(ss), _hptr(p),
+                                                  _hptr(cc) if cc is not None else None, _hptr(st)), "encaps")
+        return (c, ss, st) if return_status else (c, ss)
+
+    # ------------------------------------------------------------------ Decaps
+    def decaps(self, sk, ct_):
+        """Returns ss [n, ss_len]; implicit rejection (never fails on well-sized input)."""
+        if _is_dev(sk) and _is_dev(ct_):
+            n = sk.shape[0]
+            ss = self._empty(n, self.ss_len)
+            self._check(LIB.qrk_kem_decaps_batch(self._ctx, self._name, n, _dptr(ss), _dptr(ct_), _dptr(sk),
+                                                 self._stream()), "decaps")
+            return ss
+        s = _as_host(sk, self.sk_len)
+        c = _as_host(ct_, self.ct_len)
+        if s.shape[0] != c.shape[0]:
+            raise ValueError("sk and ct batch sizes differ")
+        ss = np.zeros((s.shape[0], self.ss_len), np.uint8)
+        self._check(LIB.qrk_kem_decaps_batch_host(self._ctx, self._name, s.shape[0], _hptr(ss), _hptr(c), _hptr(s)),
+                    "decaps")
+        return ss
+
+    # ------------------------------------------------------------------ bench helpers
+    def bench_coins(self, n: int, length: int, seed: int, first: int = 0):
+        out = self._empty(n, length)
+        self._check(LIB.qrk_bench_coins(self._ctx, n, length, seed, first, _dptr(out), self._stream()),
+                    "bench_coins")
+        return out
+
+    def tamper(self, ct_, seed: int, mode: int) -> None:
+        """In-place: mode 0 none, 1 every ciphertext, 2 Bernoulli(1/2) per index."""
+        self._check(LIB.qrk_tamper(self._ctx, ct_.shape[0], self.ct_len, seed, mode, _dptr(ct_), self._stream()),
+                    "tamper")

@@ -1,0 +1,178 @@
+"""liboqs-style KEM wrapper over libqrkem.so.
+
+Same public surface as the reference's vendored wrapper for the KEM half
+(``quantum_resistant_p2p/vendor/oqs.py:209-421``): ``KeyEncapsulation`` with
+``generate_keypair`` / ``export_secret_key`` / ``encap_secret`` /
+``decap_secret`` / ``free``, the two mechanism exceptions, and the
+``get_enabled_kem_mechanisms`` / ``get_supported_kem_mechanisms`` registry --
+so ``quantum_resistant_p2p/crypto/key_exchange.py`` runs on top of it unchanged.
+
+Differences, all deliberate:
+* the struct is not a ctypes.Structure subclass; lengths are read through the
+  C ABI (``qrk_kem_sizes``) instead of dereferencing ``OQS_KEM*``;
+* each call is one handshake on the GPU (batch of one); the batched engine is
+  :mod:`qrkem.batch`;
+* ``encap_secret(public_key)`` reproduces ctypes ``create_string_buffer``
+  semantics of the reference (``oqs.py:338-341``): a shorter key is
+  zero-padded, a longer one raises ``ValueError``.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from typing import Union
+
+from ._native import LIB, last_error
+
+OQS_SUCCESS = 0
+OQS_ERROR = -1
+
+
+def oqs_version() -> str:
+    return LIB.OQS_version().decode()
+
+
+class MechanismNotSupportedError(Exception):
+    """The algorithm name is unknown to the library (oqs.py:209-215)."""
+
+    def __init__(self, alg_name: str) -> None:
+        self.alg_name = alg_name
+        self.message = f"{alg_name} is not supported by OQS"
+        super().__init__(self.message)
+
+
+class MechanismNotEnabledError(MechanismNotSupportedError):
+    """Known to the library but without an implementation (oqs.py:218-224)."""
+
+    def __init__(self, alg_name: str) -> None:
+        super().__init__(alg_name)
+        self.message = f"{alg_name} is supported but not enabled by OQS"
+        self.args = (self.message,)
+
+
+def _names() -> tuple[str, ...]:
+    return tuple(LIB.OQS_KEM_alg_identifier(i).decode() for i in range(LIB.OQS_KEM_alg_count()))
+
+
+_SUPPORTED = _names()
+_ENABLED = tuple(n for n in _SUPPORTED if LIB.OQS_KEM_alg_is_enabled(n.encode()))
+
+
+def get_supported_kem_mechanisms() -> tuple[str, ...]:
+    return _SUPPORTED
+
+
+def get_enabled_kem_mechanisms() -> tuple[str, ...]:
+    return _ENABLED
+
+
+def is_kem_enabled(alg_name: str) -> bool:
+    return bool(LIB.OQS_KEM_alg_is_enabled(alg_name.encode()))
+
+
+def kem_sizes(alg_name: str) -> dict:
+    out = (ct.c_size_t * 6)()
+    if LIB.qrk_kem_sizes(alg_name.encode(), out) != 0:
+        raise MechanismNotSupportedError(alg_name)
+    keys = ("length_public_key", "length_secret_key", "length_ciphertext",
+            "length_shared_secret", "length_keypair_coins", "length_encaps_coins")
+    return dict(zip(keys, (int(v) for v in out)))
+
+
+_LEVEL = {"512": 1, "768": 3, "1024": 5, "640": 1, "976": 3, "1344": 5}
+
+
+def _fixed(data: Union[bytes, bytearray, memoryview], size: int) -> ct.Array:
+    # ctypes.create_string_buffer(init, size) semantics (oqs.py:294-297, 338-341)
+    return ct.create_string_buffer(bytes(data), size)
+
+
+class KeyEncapsulation:
+    """One KEM mechanism; mirrors ``oqs.KeyEncapsulation`` (oqs.py:227-393)."""
+
+    def __init__(self, alg_name: str, secret_key: Union[bytes, None] = None) -> None:
+        self.alg_name = alg_name
+        if alg_name not in _ENABLED:
+            if alg_name in _SUPPORTED:
+                raise MechanismNotEnabledError(alg_name)
+            raise MechanismNotSupportedError(alg_name)
+        self._kem = LIB.OQS_KEM_new(alg_name.encode())
+        if not self._kem:
+            raise RuntimeError(f"OQS_KEM_new({alg_name}) failed: {last_error()}")
+        sz = kem_sizes(alg_name)
+        self.method_name = alg_name.encode()
+        self.alg_version = b"qrkem-gfx950"
+        self.claimed_nist_level = _LEVEL.get(alg_name.split("-")[2 if alg_name.startswith("ML-") else 1], 0)
+        self.ind_cca = 1
+        self.length_public_key = sz["length_public_key"]
+        self.length_secret_key = sz["length_secret_key"]
+        self.length_ciphertext = sz["length_ciphertext"]
+        self.length_shared_secret = sz["length_shared_secret"]
+        self.details = {
+            "name": alg_name,
+            "version": self.alg_version.decode(),
+            "claimed_nist_level": int(self.claimed_nist_level),
+            "is_ind_cca": True,
+            "length_public_key": self.length_public_key,
+            "length_secret_key": self.length_secret_key,
+            "length_ciphertext": self.length_ciphertext,
+            "length_shared_secret": self.length_shared_secret,
+        }
+        if secret_key:
+            self.secret_key = _fixed(secret_key, self.length_secret_key)
+
+    def __enter__(self) -> "KeyEncapsulation":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.free()
+
+    def generate_keypair(self) -> bytes:
+        pk = ct.create_string_buffer(self.length_public_key)
+        self.secret_key = ct.create_string_buffer(self.length_secret_key)
+        if LIB.OQS_KEM_keypair(self._kem, pk, self.secret_key) != OQS_SUCCESS:
+            raise RuntimeError("Can not generate keypair")
+        return bytes(pk)
+
+    def generate_keypair_derand(self, coins: bytes) -> bytes:
+        """Deterministic KeyGen from explicit coins (d||z for ML-KEM)."""
+        pk = ct.create_string_buffer(self.length_public_key)
+        self.secret_key = ct.create_string_buffer(self.length_secret_key)
+        if LIB.OQS_KEM_keypair_derand(self._kem, pk, self.secret_key, bytes(coins)) != OQS_SUCCESS:
+            raise RuntimeError("Can not generate keypair")
+        return bytes(pk)
+
+    def export_secret_key(self) -> bytes:
+        return bytes(self.secret_key)
+
+    def encap_secret(self, public_key: Union[bytes, bytearray]) -> tuple[bytes, bytes]:
+        pk = _fixed(public_key, self.length_public_key)
+        c = ct.create_string_buffer(self.length_ciphertext)
+        ss = ct.create_string_buffer(self.length_shared_secret)
+        if LIB.OQS_KEM_encaps(self._kem, c, ss, pk) != OQS_SUCCESS:
+            raise RuntimeError("Can not encapsulate secret")
+        return bytes(c), bytes(ss)
+
+    def encap_secret_derand(self, public_key: bytes, coins: bytes) -> tuple[bytes, bytes]:
+        pk = _fixed(public_key, self.length_public_key)
+        c = ct.create_string_buffer(self.length_ciphertext)
+        ss = ct.create_string_buffer(self.length_shared_secret)
+        if LIB.OQS_KEM_encaps_derand(self._kem, c, ss, pk, bytes(coins)) != OQS_SUCCESS:
+            raise RuntimeError("Can not encapsulate secret")
+        return bytes(c), bytes(ss)
+
+    def decap_secret(self, ciphertext: Union[bytes, bytearray]) -> bytes:
+        c = _fixed(ciphertext, self.length_ciphertext)
+        ss = ct.create_string_buffer(self.length_shared_secret)
+        if LIB.OQS_KEM_decaps(self._kem, ss, c, self.secret_key) != OQS_SUCCESS:
+            raise RuntimeError("Can not decapsulate secret")
+        return bytes(ss)
+
+    def free(self) -> None:
+        if getattr(self, "secret_key", None) is not None:
+            LIB.OQS_MEM_cleanse(ct.addressof(self.secret_key), self.length_secret_key)
+        if self._kem:
+            LIB.OQS_KEM_free(self._kem)
+            self._kem = None
+
+    def __repr__(self) -> str:
+        return f"Key encapsulation mechanism: {self.alg_name}"

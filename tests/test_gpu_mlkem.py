@@ -1,0 +1,148 @@
+"""HIP ML-KEM parity vs the oracle, through the C ABI (libqrkem.so).
+
+Bar: byte-exact pk / sk / ct / ss for every index (integer work).
+Sizes are ragged on purpose (not multiples of the 16-handshake workgroup or
+the 64-instance scratch tile).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+ALGS = ["ML-KEM-512", "ML-KEM-768", "ML-KEM-1024"]
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from qrkem.batch import BatchKEM
+    return {a: BatchKEM(a, device=0) for a in ALGS}
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("n", [1, 17, 301])
+def test_roundtrip_matches_oracle(engines, alg, n):
+    import oracle as orc
+    eng = engines[alg]
+    coins = orc.bench_coins(n, 96, seed=1234 + n)
+    kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
+    pk, sk = eng.keypair(coins=_dev(kc))
+    ct, ss = eng.encaps(pk, coins=_dev(ec))
+    ss2 = eng.decaps(sk, ct)
+    pk, sk, ct, ss, ss2 = map(_host, (pk, sk, ct, ss, ss2))
+    opk, osk = orc.batch_keypair(alg, kc)
+    assert np.array_equal(pk, opk)
+    assert np.array_equal(sk, osk)
+    oct_, oss = orc.batch_encaps(alg, opk, ec)
+    assert np.array_equal(ct, oct_)
+    assert np.array_equal(ss, oss)
+    assert np.array_equal(ss2, oss)
+
+
+@pytest.mark.parametrize("alg", ALGS)
+def test_tampered_implicit_rejection(engines, alg):
+    import oracle as orc
+    eng = engines[alg]
+    n = 130
+    coins = orc.bench_coins(n, 96, seed=99)
+    kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
+    opk, osk = orc.batch_keypair(alg, kc)
+    oct_, oss = orc.batch_encaps(alg, opk, ec)
+    bad = oct_.copy()
+    rng = np.random.default_rng(7)
+    flip = rng.random(n) < 0.5
+    for i in np.nonzero(flip)[0]:
+        bit = int(rng.integers(0, 8 * bad.shape[1]))
+        bad[i, bit // 8] ^= 1 << (bit % 8)
+    ss = _host(eng.decaps(_dev(osk), _dev(bad)))
+    want = orc.batch_decaps(alg, osk, bad)
+    assert np.array_equal(ss, want)
+    assert np.array_equal(ss[~flip], oss[~flip])
+    assert not np.any(np.all(ss[flip] == oss[flip], axis=1))
+
+
+@pytest.mark.parametrize("alg", ALGS)
+def test_host_pointer_api(engines, alg):
+    import oracle as orc
+    eng = engines[alg]
+    coins = orc.bench_coins(5, 96, seed=5)
+    kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
+    pk, sk = eng.keypair(coins=kc)
+    ct, ss, st = eng.encaps(pk, coins=ec, return_status=True)
+    assert np.all(st == 0)
+    opk, osk = orc.batch_keypair(alg, kc)
+    oct_, oss = orc.batch_encaps(alg, opk, ec)
+    assert np.array_equal(pk, opk) and np.array_equal(sk, osk)
+    assert np.array_equal(ct, oct_) and np.array_equal(ss, oss)
+    assert np.array_equal(eng.decaps(sk, ct), oss)
+
+
+def test_modulus_check_status(engines):
+    import oracle as orc
+    alg = "ML-KEM-768"
+    eng = engines[alg]
+    coins = orc.bench_coins(4, 96, seed=11)
+    opk, _ = orc.batch_keypair(alg, np.ascontiguousarray(coins[:, :64]))
+    pk = opk.copy()
+    pk[1, 0] = 0xFF
+    pk[1, 1] |= 0x0F  # first coefficient = 4095 >= q
+    _, _, st = eng.encaps(_dev(pk), coins=_dev(np.ascontiguousarray(coins[:, 64:])), return_status=True)
+    st = _host(st)
+    assert list(st) == [0, -1, 0, 0]
+
+
+def test_single_shot_oqs_api():
+    import oracle as orc
+    from qrkem import oqs
+    alg = "ML-KEM-768"
+    kc = bytes(range(64))
+    ec = bytes(range(100, 132))
+    k = oqs.KeyEncapsulation(alg)
+    pk = k.generate_keypair_derand(kc)
+    sk = k.export_secret_key()
+    opk, osk = orc.keypair(alg, kc)
+    assert pk == opk and sk == osk
+    c, ss = oqs.KeyEncapsulation(alg).encap_secret_derand(pk, ec)
+    oc, oss = orc.encaps(alg, pk, ec)
+    assert c == oc and ss == oss
+    assert oqs.KeyEncapsulation(alg, sk).decap_secret(c) == oss
+    # random (OS CSPRNG) path round-trips
+    pk2 = k.generate_keypair()
+    c2, s2 = oqs.KeyEncapsulation(alg).encap_secret(pk2)
+    assert oqs.KeyEncapsulation(alg, k.export_secret_key()).decap_secret(c2) == s2
+
+
+def test_bench_coins_device_matches_oracle(engines):
+    import oracle as orc
+    eng = engines["ML-KEM-768"]
+    got = _host(eng.bench_coins(1000, 96, seed=0x5EED, first=12345))
+    assert np.array_equal(got, orc.bench_coins(1000, 96, 0x5EED, 12345))
+
+
+def test_tamper_kernel_matches_definition(engines):
+    eng = engines["ML-KEM-768"]
+    n, L = 200, 1088
+    base = np.zeros((n, L), np.uint8)
+    t = _dev(base)
+    eng.tamper(t, seed=77, mode=2)
+    got = _host(t)
+    for i in range(n):
+        h = int.from_bytes(hashlib.shake_256(b"qrk-tamper" + (77).to_bytes(8, "little")
+                                             + i.to_bytes(8, "little")).digest(8), "little")
+        want = np.zeros(L, np.uint8)
+        if h & 1:
+            bit = (h >> 1) % (8 * L)
+            want[bit // 8] = 1 << (bit % 8)
+        assert np.array_equal(got[i], want), i
