@@ -127,6 +127,14 @@ int qrk_bench_coins(qrk_ctx *ctx, size_t n, size_t len, uint64_t seed, uint64_t 
  * h_i = SHAKE256("qrk-tamper"||LE64(seed)||LE64(i))[0..8), bit (h_i>>1) mod 8*ctlen. */
 int qrk_tamper(qrk_ctx *ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t *ct, void *stream);
 
+/* Per-kernel HIP-event timing on the launch stream (for bench.py's roofline).
+ * qrk_ctx_profile(ctx, 1) resets and enables; qrk_ctx_profile_collect()
+ * synchronises the recorded events and returns the number of distinct kernel
+ * names; qrk_ctx_profile_get() reads (name, total ms, launches) for entry i. */
+int qrk_ctx_profile(qrk_ctx *ctx, int enable);
+int qrk_ctx_profile_collect(qrk_ctx *ctx);
+int qrk_ctx_profile_get(qrk_ctx *ctx, int i, const char **name, double *total_ms, uint64_t *launches);
+
 const char *qrk_last_error(void);
 int qrk_device_count(void);
 

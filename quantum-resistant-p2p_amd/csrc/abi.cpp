@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/qrkem.h"
 #include "qrkem_internal.h"
@@ -64,10 +65,58 @@ static int hip_fail(const char* what, hipError_t e) {
   return fail(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// ------------------------------------------------------------------ kernel timing
+namespace qrk {
+thread_local KernelTimer* g_timer = nullptr;
+}
+
+// Pairs of HIP events recorded on the launch stream around every kernel; read
+// back (after a synchronise) as per-kernel-name totals.
+struct EventTimer : KernelTimer {
+  struct Rec {
+    const char* name;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t pending = nullptr;
+  hipEvent_t take() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void before(const char*, hipStream_t st) override {
+    pending = take();
+    (void)hipEventRecord(pending, st);
+  }
+  void after(const char* name, hipStream_t st) override {
+    hipEvent_t b = take();
+    (void)hipEventRecord(b, st);
+    recs.push_back({name, pending, b});
+    pending = nullptr;
+  }
+  void reset() {
+    for (auto& r : recs) pool.push_back(r.a), pool.push_back(r.b);
+    recs.clear();
+  }
+  ~EventTimer() override {
+    reset();
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
 // ------------------------------------------------------------------ context
 struct qrk_ctx {
   int device = 0;
   size_t chunk = 1 << 16;
+  bool profiling = false;
+  EventTimer timer;
+  std::vector<std::pair<std::string, std::pair<double, uint64_t>>> profile;  // name -> (ms, launches)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   uint8_t* dstage = nullptr;  // device staging for host-pointer calls and generated coins
@@ -163,6 +212,10 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     coins = ctx->dstage;
     synth = true;
   }
+  struct TimerScope {
+    explicit TimerScope(KernelTimer* t) { g_timer = t; }
+    ~TimerScope() { g_timer = nullptr; }
+  } timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     hipError_t e = hipSuccess;
@@ -399,6 +452,45 @@ int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {
 }
 
 size_t qrk_ctx_scratch_bytes(const qrk_ctx* ctx) { return ctx ? ctx->scratch_bytes : 0; }
+
+int qrk_ctx_profile(qrk_ctx* ctx, int enable) {
+  if (!ctx) return fail("null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->timer.reset();
+  ctx->profile.clear();
+  ctx->profiling = enable != 0;
+  return 0;
+}
+
+int qrk_ctx_profile_collect(qrk_ctx* ctx) {
+  if (!ctx) return fail("null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (auto& r : ctx->timer.recs) {
+    hipError_t e = hipEventSynchronize(r.b);
+    if (e != hipSuccess) return hip_fail("hipEventSynchronize", e);
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, r.a, r.b);
+    if (e != hipSuccess) return hip_fail("hipEventElapsedTime", e);
+    auto it = std::find_if(ctx->profile.begin(), ctx->profile.end(),
+                           [&](const auto& p) { return p.first == r.name; });
+    if (it == ctx->profile.end()) {
+      ctx->profile.push_back({r.name, {ms, 1}});
+    } else {
+      it->second.first += ms;
+      it->second.second += 1;
+    }
+  }
+  ctx->timer.reset();
+  return (int)ctx->profile.size();
+}
+
+int qrk_ctx_profile_get(qrk_ctx* ctx, int i, const char** name, double* total_ms, uint64_t* launches) {
+  if (!ctx || i < 0 || i >= (int)ctx->profile.size()) return fail("profile index out of range");
+  *name = ctx->profile[i].first.c_str();
+  *total_ms = ctx->profile[i].second.first;
+  *launches = ctx->profile[i].second.second;
+  return 0;
+}
 
 int qrk_kem_sizes(const char* alg, size_t out[6]) {
   const AlgInfo* a = find_alg(alg);

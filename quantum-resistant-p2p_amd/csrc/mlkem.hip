@@ -904,14 +904,14 @@ template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  hipLaunchKernelGGL(k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk, v.seeds);
-  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds, n,
+  QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk, v.seeds);
+  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds, n,
                      C, 2 * K, 2 * K, v.prf);
-  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
+  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
                      (size_t)P<K>::PK, n, C, v.xof);
-  hipLaunchKernelGGL(k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C, v.xof,
+  QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C, v.xof,
                      v.prf, pk, sk);
-  hipLaunchKernelGGL(k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
+  QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
 
@@ -920,12 +920,12 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
                        int32_t* status, void* scratch, hipStream_t st) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  hipLaunchKernelGGL(k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss, v.seeds);
-  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+  QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss, v.seeds);
+  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
                      v.seeds, n, C, 2 * K + 1, K, v.prf);
-  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
+  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
                      (size_t)P<K>::PK, n, C, v.xof);
-  hipLaunchKernelGGL((k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C,
+  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C,
                      v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr, nullptr);
   return hipGetLastError();
 }
@@ -935,14 +935,14 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
-  hipLaunchKernelGGL(k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-  hipLaunchKernelGGL(k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n, v.seeds,
+  QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
+  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n, v.seeds,
                      v.kprime, v.kbar);
-  hipLaunchKernelGGL((k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
                      v.seeds, n, C, 2 * K + 1, K, v.prf);
-  hipLaunchKernelGGL(k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, sk + 768 * K,
+  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, sk + 768 * K,
                      (size_t)P<K>::SK, n, C, v.xof);
-  hipLaunchKernelGGL((k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf, sk + 384 * K,
+  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf, sk + 384 * K,
                      (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
                      (int32_t*)nullptr, v.kprime, v.kbar, ss);
   return hipGetLastError();

@@ -24,6 +24,23 @@ const AlgInfo* find_alg(const char* name);
 int alg_count();
 const AlgInfo* alg_at(int i);
 
+// Optional per-kernel HIP-event timing (qrk_ctx_profile): when a context has
+// profiling enabled, every QRK_LAUNCH brackets the launch with two events on the
+// launch stream; durations are summed per kernel name.
+struct KernelTimer {
+  virtual void before(const char* name, hipStream_t st) = 0;
+  virtual void after(const char* name, hipStream_t st) = 0;
+  virtual ~KernelTimer() = default;
+};
+extern thread_local KernelTimer* g_timer;
+
+#define QRK_LAUNCH(NAME, ST, ...)                   \
+  do {                                              \
+    if (::qrk::g_timer) ::qrk::g_timer->before(NAME, ST); \
+    hipLaunchKernelGGL(__VA_ARGS__);                \
+    if (::qrk::g_timer) ::qrk::g_timer->after(NAME, ST);  \
+  } while (0)
+
 // Device scratch owned by a context.  Grown on demand, never shrunk.
 struct Scratch {
   void* base = nullptr;

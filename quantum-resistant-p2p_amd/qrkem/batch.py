@@ -161,6 +161,24 @@ class BatchKEM:
                     "decaps")
         return ss
 
+    # ------------------------------------------------------------------ kernel timing
+    def profile(self, enable: bool = True) -> None:
+        """Reset and enable/disable per-kernel HIP-event timing on the launch stream."""
+        self._check(LIB.qrk_ctx_profile(self._ctx, int(enable)), "profile")
+
+    def profile_read(self) -> dict:
+        """{kernel name: (total ms, launches)} accumulated since profile(True)."""
+        n = LIB.qrk_ctx_profile_collect(self._ctx)
+        if n < 0:
+            raise RuntimeError(f"qrkem profile collect failed: {last_error()}")
+        out = {}
+        for i in range(n):
+            name, ms, cnt = ct.c_char_p(), ct.c_double(), ct.c_uint64()
+            self._check(LIB.qrk_ctx_profile_get(self._ctx, i, ct.byref(name), ct.byref(ms), ct.byref(cnt)),
+                        "profile_get")
+            out[name.value.decode()] = (ms.value, cnt.value)
+        return out
+
     # ------------------------------------------------------------------ bench helpers
     def bench_coins(self, n: int, length: int, seed: int, first: int = 0):
         out = self._empty(n, length)
