@@ -28,7 +28,7 @@ namespace mlkem {
 
 constexpr int Q = 3329;
 constexpr int QINV = 62209;  // q^-1 mod 2^16
-constexpr int XOF_W = 84;    // four SHAKE128 blocks (168 B) of raw XOF output
+constexpr int XOF_W = 64;    // 256 int16 sampled coefficients (512 B) per matrix entry
 constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
 constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
 constexpr int R2 = 1353;       // R^2 mod q            (to Montgomery form)
@@ -116,28 +116,31 @@ __device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, i
   c[7] = (int)(w2 >> 20);
 }
 
-__device__ __forceinline__ int count_lt_q(uint32_t w0, uint32_t w1, uint32_t w2) {
-  int c[8];
-  split12(w0, w1, w2, c);
-  int n = 0;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) n += c[e] < Q;
-  return n;
-}
-
 // ============================================================ lane-per-instance Keccak kernels
 
-// SampleNTT producer: SHAKE128(rho || x || y), 3 squeezed blocks (+ a 4th when
-// the first 504 bytes hold fewer than 256 values < q), raw words to scratch.
-// inst = (x*K + y) * C + hs.
+// SampleNTT (FIPS 203 Alg. 7), one lane per matrix entry: SHAKE128(rho || x || y)
+// squeezed block by block until 256 values < q have been accepted (3 blocks
+// with probability ~0.993, rarely 4).  Compaction happens in the producer:
+// every candidate is written to a 16-entry per-lane LDS ring at the running
+// count (a rejected one is simply overwritten by the next), and each completed
+// 8-coefficient chunk is flushed as one 16-byte store.  Output: 256 int16
+// coefficients per entry in a 64-entry tiled layout (chunk c of entry i at
+// ((i/64)*32 + c)*64 + i%64, 16-byte units), so the consumer reads them
+// without any parsing.  inst = (x*K + y) * C + hs.
+constexpr int RING_DW = 10;  // per-lane ring stride in dwords (40 B: 8-B aligned, 2-way banked)
+constexpr int MAX_XOF_BLOCKS = 8;
+
 template <int K>
 __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
-                                             size_t n, size_t C, uint64_t* __restrict__ xof) {
+                                             size_t n, size_t C, uint4* __restrict__ out) {
+  __shared__ uint32_t ring_all[256 * RING_DW];
   const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (inst >= (size_t)K * K * C) return;
   const size_t hs = inst % C;
   const int xy = (int)(inst / C);
   if (hs >= n) return;
+  uint16_t* ring = (uint16_t*)(ring_all + threadIdx.x * RING_DW);
+  uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
   const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
   KState s;
   kzero(s);
@@ -147,22 +150,30 @@ __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_bas
   s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
   int cnt = 0;
 #pragma unroll 1
-  for (int b = 0; b < 4; ++b) {
-    if (b == 3 && cnt >= 256) break;
+  for (int b = 0; b < MAX_XOF_BLOCKS && cnt < 256; ++b) {
     keccak_f(s);
+    // 42 dwords = 14 triplets of 8 twelve-bit candidates
 #pragma unroll
-    for (int w = 0; w < RW_SHAKE128; ++w) xof[tidx(inst, b * RW_SHAKE128 + w, XOF_W)] = kword(s, w);
-    if (b < 3) {
-      // 42 dwords = 14 triplets of 8 candidates
+    for (int t = 0; t < 14; ++t) {
+      uint32_t d[3];
 #pragma unroll
-      for (int t = 0; t < 14; ++t) {
-        uint32_t d[3];
+      for (int e = 0; e < 3; ++e) {
+        const int di = 3 * t + e;
+        d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
+      }
+      int c[8];
+      split12(d[0], d[1], d[2], c);
+      const int before = cnt;
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          const int di = 3 * t + e;
-          d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
-        }
-        cnt += count_lt_q(d[0], d[1], d[2]);
+      for (int e = 0; e < 8; ++e) {
+        ring[cnt & 15] = (uint16_t)c[e];
+        cnt += c[e] < Q;
+      }
+      const int ch = before >> 3;
+      if ((cnt >> 3) != ch && ch < 32) {
+        const uint2 lo = *(const uint2*)(ring + (ch & 1) * 8);
+        const uint2 hi = *(const uint2*)(ring + (ch & 1) * 8 + 4);
+        dst[ch * 64] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
     }
   }
@@ -445,19 +456,46 @@ __device__ __forceinline__ void ntt_inv(P16& p, int* buf, int L) {
   for (int m = 0; m < 16; ++m) p.v[m] = fqmul(p.v[m], F_SCALE);
 }
 
-// b1*gamma for the 8 coefficient pairs of a contiguous NTT-domain operand
-__device__ __forceinline__ void pair_gamma(const P16& b, int g[8], int L) {
-#pragma unroll
-  for (int u = 0; u < 8; ++u) g[u] = fqmul(b.v[2 * u + 1], TABD.gm[8 * L + u]);
+// ---- base-case multiplication (FIPS 203 Alg. 11/12) on packed int16 pairs
+// A coefficient pair (a0, a1) lives in one dword (lo, hi) -- exactly the
+// producer's sampled layout.  For the other operand b we precompute
+//   B0 = (b0, b1*gamma)   and   B1 = (b1, b0)
+// so that  c0 = a0 b0 + a1 b1 gamma = dot2(A, B0),  c1 = a0 b1 + a1 b0 = dot2(A, B1):
+// two v_dot2c_i32_i16 per pair, accumulated unreduced over the k terms.
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+struct PK8 {  // 16 coefficients as 8 packed int16 pairs (contiguous layout)
+  uint32_t w[8];
+};
+struct BOp {  // basemul right operand
+  uint32_t b0[8], b1[8];
+};
+
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) {
+  return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
 }
 
-// acc += a o b   (a in [0,q), b and bg centered): 4 mad24 per pair, reduced later
-__device__ __forceinline__ void basemul_acc(int acc[16], const P16& a, const P16& b, const int bg[8]) {
+__device__ __forceinline__ BOp make_bop(const P16& b, int L) {
+  BOp r;
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    const int a0 = a.v[2 * u], a1 = a.v[2 * u + 1];
-    acc[2 * u] += __mul24(a0, b.v[2 * u]) + __mul24(a1, bg[u]);
-    acc[2 * u + 1] += __mul24(a0, b.v[2 * u + 1]) + __mul24(a1, b.v[2 * u]);
+    const int g = fqmul(b.v[2 * u + 1], TABD.gm[8 * L + u]);
+    r.b0[u] = pack16(b.v[2 * u], g);
+    r.b1[u] = pack16(b.v[2 * u + 1], b.v[2 * u]);
+  }
+  return r;
+}
+
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c, false);
+}
+
+// acc += a o b  (a in [0, q), b centered; |acc| stays < 2^27 for k <= 4)
+__device__ __forceinline__ void basemul_acc(int acc[16], const PK8& a, const BOp& b) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    acc[2 * u] = dot2(a.w[u], b.b0[u], acc[2 * u]);
+    acc[2 * u + 1] = dot2(a.w[u], b.b1[u], acc[2 * u + 1]);
   }
 }
 
@@ -569,76 +607,31 @@ __device__ __forceinline__ void flush_bits(GroupLds& g, uint8_t* dst, const uint
   gsync();
 }
 
-// SampleNTT consumer: copy the raw XOF words of `inst` to LDS, compact values < q
-// in stream order (group prefix sums), return the polynomial in contiguous layout.
-__device__ __forceinline__ void sample_ntt(P16& a, const uint64_t* __restrict__ xof, size_t inst, GroupLds& g,
-                                           int L) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int w = L + 16 * i;
-    if (w < 63) g.raw[w] = xof[tidx(inst, w, XOF_W)];
-  }
-  gsync();
-  const uint32_t* r32 = (const uint32_t*)g.raw;
-  int total = 0;
-#pragma unroll 1
-  for (int blk = 0; blk < 4; ++blk) {
-    if (blk == 3) {
-      if (total >= 256) break;
-      // rare: fourth block (producer squeezed it for exactly this case)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int w = 63 + L + 16 * i;
-        if (w < 84) g.raw[w] = xof[tidx(inst, w, XOF_W)];
-      }
-      gsync();
-    }
-    int c[8];
-    const bool lane_ok = L < 14;
-    const int d0 = 42 * blk + 3 * L;
-    if (lane_ok) {
-      split12(r32[d0], r32[d0 + 1], r32[d0 + 2], c);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) c[e] = Q;
-    }
-    int cnt = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) cnt += c[e] < Q;
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      const int o = __shfl_up(incl, d, 16);
-      if (L >= d) incl += o;
-    }
-    int pos = total + incl - cnt;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (c[e] < Q) {
-        if (pos < 256) g.poly[pos + (pos >> 4)] = c[e];
-        ++pos;
-      }
-    }
-    total += __shfl(incl, 15, 16);
-  }
-  gsync();
-#pragma unroll
-  for (int t = 0; t < 16; ++t) a.v[t] = g.poly[17 * L + t];
-  gsync();
+// SampleNTT consumer: lane L loads coefficients 16L..16L+15 (chunks 2L, 2L+1)
+// of the producer's compacted output -- contiguous layout, no parsing.
+__device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t inst, int L) {
+  const uint4* base = xs + (inst >> 6) * 32 * 64 + (inst & 63);
+  const uint4 u = base[(2 * L) * 64], v = base[(2 * L + 1) * 64];
+  return PK8{{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}};
 }
 
-// 12-bit decode of a 384-byte encoded NTT-domain polynomial; optional modulus check.
-__device__ __forceinline__ void decode12(P16& p, const uint8_t* __restrict__ src, bool& bad, int L) {
+// ByteDecode_12 (reduced mod q) of a 384-byte NTT-domain polynomial into packed
+// pairs; `bad` collects the FIPS 203 section 7.2 modulus-check failure.
+__device__ __forceinline__ PK8 decode12(const uint8_t* __restrict__ src, bool& bad, int L) {
   const uint64_t* s = (const uint64_t*)(src + 24 * L);
   const uint64_t a = s[0], b = s[1], c = s[2];
   int v[16];
   split12((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, v);
   split12((uint32_t)(b >> 32), (uint32_t)c, (uint32_t)(c >> 32), v + 8);
+  PK8 r;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     bad |= v[t] >= Q;
-    p.v[t] = v[t] >= Q ? v[t] - Q : v[t];
+    v[t] = v[t] >= Q ? v[t] - Q : v[t];
   }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) r.w[u] = pack16(v[2 * u], v[2 * u + 1]);
+  return r;
 }
 
 __device__ __forceinline__ void encode12(const P16& p, uint8_t* dst, int L) {
@@ -701,25 +694,19 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
   const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
-  P16 sh[K];
-  int sg[K][8];
+  uint8_t* ek = pk + hs * P<K>::PK;
+  uint8_t* dk = sk + hs * P<K>::SK;
+  BOp sb[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     P16 t;
     cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
     contig_to_stride(t, g.poly, L);
     ntt_fwd(t, g.poly, L);
-    sh[j] = t;
-    pair_gamma(t, sg[j], L);
-  }
-  uint8_t* ek = pk + hs * P<K>::PK;
-  uint8_t* dk = sk + hs * P<K>::SK;
+    sb[j] = make_bop(t, L);
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    P16 s;
-#pragma unroll
-    for (int x = 0; x < 16; ++x) s.v[x] = canon(sh[j].v[x]);
-    if (active) encode12(s, dk + 384 * j, L);
+    for (int x = 0; x < 16; ++x) t.v[x] = canon(t.v[x]);
+    if (active) encode12(t, dk + 384 * j, L);
   }
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
@@ -728,9 +715,7 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
     for (int t = 0; t < 16; ++t) acc[t] = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      P16 a;
-      sample_ntt(a, xof, (size_t)(j * K + i) * C + hs, g, L);
-      basemul_acc(acc, a, sh[j], sg[j]);
+      basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(j * K + i) * C + hs, L), sb[j]);
     }
     P16 e;
     cbd<P<K>::ETA1>(e, prf, (size_t)(K + i) * C + hs, L);
@@ -768,16 +753,14 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
 
-  P16 yh[K];
-  int yg[K][8];
+  BOp yb[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     P16 t;
     cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
     contig_to_stride(t, g.poly, L);
     ntt_fwd(t, g.poly, L);
-    yh[j] = t;
-    pair_gamma(t, yg[j], L);
+    yb[j] = make_bop(t, L);
   }
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j)
 #pragma unroll 1
@@ -787,9 +770,7 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
     for (int t = 0; t < 16; ++t) acc[t] = 0;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      P16 a;
-      sample_ntt(a, xof, (size_t)(i * K + j) * C + hs, g, L);
-      basemul_acc(acc, a, yh[j], yg[j]);
+      basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(i * K + j) * C + hs, L), yb[j]);
     }
     P16 u;
 #pragma unroll
@@ -811,9 +792,7 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      P16 th;
-      decode12(th, ek + 384 * j, bad, L);
-      basemul_acc(acc, th, yh[j], yg[j]);
+      basemul_acc(acc, decode12(ek + 384 * j, bad, L), yb[j]);
     }
     P16 v;
 #pragma unroll
@@ -873,11 +852,7 @@ __global__ __launch_bounds__(256) void k_decrypt_core(size_t n, const uint8_t* _
     for (int t = 0; t < 16; ++t) u.v[t] = decompress<DU>(u.v[t]);
     contig_to_stride(u, g.poly, L);
     ntt_fwd(u, g.poly, L);
-    int ug[8];
-    pair_gamma(u, ug, L);
-    P16 s;
-    decode12(s, dk + 384 * j, bad, L);
-    basemul_acc(acc, s, u, ug);
+    basemul_acc(acc, decode12(dk + 384 * j, bad, L), make_bop(u, L));
   }
   P16 w;
 #pragma unroll
@@ -908,7 +883,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds, n,
                      C, 2 * K, 2 * K, v.prf);
   QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
-                     (size_t)P<K>::PK, n, C, v.xof);
+                     (size_t)P<K>::PK, n, C, (uint4*)v.xof);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C, v.xof,
                      v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
@@ -924,7 +899,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
                      v.seeds, n, C, 2 * K + 1, K, v.prf);
   QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
-                     (size_t)P<K>::PK, n, C, v.xof);
+                     (size_t)P<K>::PK, n, C, (uint4*)v.xof);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C,
                      v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr, nullptr);
   return hipGetLastError();
@@ -941,7 +916,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
                      v.seeds, n, C, 2 * K + 1, K, v.prf);
   QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, sk + 768 * K,
-                     (size_t)P<K>::SK, n, C, v.xof);
+                     (size_t)P<K>::SK, n, C, (uint4*)v.xof);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf, sk + 384 * K,
                      (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
                      (int32_t*)nullptr, v.kprime, v.kbar, ss);
