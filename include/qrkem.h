@@ -93,6 +93,10 @@ void qrk_ctx_destroy(qrk_ctx *ctx);
 /* Handshakes per internal chunk (scratch = chunk * per-handshake bytes). */
 int qrk_ctx_set_chunk(qrk_ctx *ctx, size_t chunk);
 size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
+/* 2 (default): independent kernel chains of one operation run forked on a
+ * side stream and join the caller's stream; 1: everything on the caller's
+ * stream (kernel timings in isolation). */
+int qrk_ctx_set_streams(qrk_ctx *ctx, int streams);
 
 /* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */
 int qrk_kem_sizes(const char *alg, size_t out[6]);

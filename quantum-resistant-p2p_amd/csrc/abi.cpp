@@ -113,7 +113,7 @@ struct EventTimer : KernelTimer {
 // ------------------------------------------------------------------ context
 struct qrk_ctx {
   int device = 0;
-  size_t chunk = 1 << 16;
+  size_t chunk = 1 << 20;
   bool profiling = false;
   EventTimer timer;
   std::vector<std::pair<std::string, std::pair<double, uint64_t>>> profile;  // name -> (ms, launches)
@@ -123,6 +123,9 @@ struct qrk_ctx {
   size_t dstage_bytes = 0;
   uint8_t* hstage = nullptr;  // pinned host staging
   size_t hstage_bytes = 0;
+  hipStream_t aux = nullptr;  // side stream for independent kernel chains
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int streams = 2;            // 1: serial schedule (kernel timings in isolation), 2: forked
   std::mutex mu;
 };
 
@@ -212,6 +215,17 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     coins = ctx->dstage;
     synth = true;
   }
+  if (!ctx->aux) {
+    hipError_t e1 = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    hipError_t e2 = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+    hipError_t e3 = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail("cannot create side stream/events");
+  }
+  Streams S;
+  S.main = st;
+  S.aux = ctx->streams > 1 ? ctx->aux : nullptr;
+  S.fork = ctx->ev_fork;
+  S.join = ctx->ev_join;
   struct TimerScope {
     explicit TimerScope(KernelTimer* t) { g_timer = t; }
     ~TimerScope() { g_timer = nullptr; }
@@ -222,27 +236,27 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     if (a.family == Family::MLKEM) {
       switch (op) {
         case Op::KEYPAIR:
-          e = mlkem_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, st);
+          e = mlkem_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, S);
           break;
         case Op::ENCAPS:
           e = mlkem_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
-                           status ? status + off : nullptr, ctx->scratch, st);
+                           status ? status + off : nullptr, ctx->scratch, S);
           break;
         case Op::DECAPS:
-          e = mlkem_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, st);
+          e = mlkem_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
           break;
       }
     } else {
       switch (op) {
         case Op::KEYPAIR:
-          e = frodo_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, st);
+          e = frodo_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, S);
           break;
         case Op::ENCAPS:
           e = frodo_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
-                           ctx->scratch, st);
+                           ctx->scratch, S);
           break;
         case Op::DECAPS:
-          e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, st);
+          e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
           break;
       }
     }
@@ -435,14 +449,24 @@ int qrk_ctx_create(qrk_ctx** out, int device) {
 
 void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->scratch || ctx->dstage) {
+  if (ctx->scratch || ctx->dstage || ctx->aux) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
   }
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
   delete ctx;
+}
+
+int qrk_ctx_set_streams(qrk_ctx* ctx, int streams) {
+  if (!ctx || streams < 1 || streams > 2) return fail("streams must be 1 or 2");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->streams = streams;
+  return 0;
 }
 
 int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {

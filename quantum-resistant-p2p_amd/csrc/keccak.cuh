@@ -132,18 +132,26 @@ __device__ __forceinline__ uint64_t kword(const KState& s, int i) {
 // Absorb a message of NW 64-bit words (little-endian) produced by `ld(w)`,
 // then pad with domain byte DS at byte offset 8*NW.  RW = rate in words.
 // NW is a compile-time constant so every state index is static.
+// The next block's words are loaded into registers before the current block's
+// permutation runs, so global-load latency hides behind the 24 rounds.
 template <int RW, int NW, uint32_t DS, typename Loader>
 __device__ __forceinline__ void absorb_words(KState& s, Loader ld) {
   constexpr int NFULL = NW / RW;
   constexpr int TAIL = NW % RW;
+  uint64_t nxt[RW];
+#pragma unroll
+  for (int w = 0; w < RW; ++w) nxt[w] = (NFULL > 0 || w < TAIL) ? ld(w) : 0;
 #pragma unroll 1
   for (int b = 0; b < NFULL; ++b) {
 #pragma unroll
-    for (int w = 0; w < RW; ++w) kxor(s, w, ld(b * RW + w));
+    for (int w = 0; w < RW; ++w) kxor(s, w, nxt[w]);
+    const int nb = (b + 1) * RW;
+#pragma unroll
+    for (int w = 0; w < RW; ++w) nxt[w] = (b + 1 < NFULL || w < TAIL) ? ld(nb + w) : 0;
     keccak_f(s);
   }
 #pragma unroll
-  for (int w = 0; w < TAIL; ++w) kxor(s, w, ld(NFULL * RW + w));
+  for (int w = 0; w < TAIL; ++w) kxor(s, w, nxt[w]);
   s.a[TAIL].lo ^= DS;
   s.a[RW - 1].hi ^= 0x80000000u;
   keccak_f(s);

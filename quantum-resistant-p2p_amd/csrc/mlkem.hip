@@ -128,53 +128,73 @@ __device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, i
 // ((i/64)*32 + c)*64 + i%64, 16-byte units), so the consumer reads them
 // without any parsing.  inst = (x*K + y) * C + hs.
 constexpr int RING_DW = 10;  // per-lane ring stride in dwords (40 B: 8-B aligned, 2-way banked)
-constexpr int MAX_XOF_BLOCKS = 8;
+constexpr int MAX_XOF_BLOCKS = 16;
 
-template <int K>
+// Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
+// flushing completed 8-coefficient chunks to dst.
+__device__ __forceinline__ void compact_block(const KState& s, uint16_t* ring, int& cnt, uint4* dst) {
+#pragma unroll
+  for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
+    uint32_t d[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const int di = 3 * t + e;
+      d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
+    }
+    int c[8];
+    split12(d[0], d[1], d[2], c);
+    const int before = cnt;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ring[cnt & 15] = (uint16_t)c[e];
+      cnt += c[e] < Q;
+    }
+    const int ch = before >> 3;
+    if ((cnt >> 3) != ch && ch < 32) {
+      const uint2 lo = *(const uint2*)(ring + (ch & 1) * 8);
+      const uint2 hi = *(const uint2*)(ring + (ch & 1) * 8 + 4);
+      dst[ch * 64] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+  }
+}
+
+// FIX == false: every entry squeezes exactly 3 blocks (uniform across the
+// wave); the ~0.7% that still lack 256 values append their index to `fix`.
+// FIX == true: one lane per listed entry recomputes it with as many blocks as
+// it needs (rewriting identical chunks), so the rare 4th block never idles a
+// whole wave.
+template <int K, bool FIX>
 __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
-                                             size_t n, size_t C, uint4* __restrict__ out) {
+                                             size_t n, size_t C, uint4* __restrict__ out,
+                                             uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
   __shared__ uint32_t ring_all[256 * RING_DW];
-  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (inst >= (size_t)K * K * C) return;
-  const size_t hs = inst % C;
-  const int xy = (int)(inst / C);
-  if (hs >= n) return;
   uint16_t* ring = (uint16_t*)(ring_all + threadIdx.x * RING_DW);
-  uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
-  const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
-  KState s;
-  kzero(s);
-#pragma unroll
-  for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
-  s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
-  s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
-  int cnt = 0;
+  const size_t stride = FIX ? (size_t)gridDim.x * 256 : 0;
+  size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t limit = FIX ? (size_t)*nfix : (size_t)K * K * C;
 #pragma unroll 1
-  for (int b = 0; b < MAX_XOF_BLOCKS && cnt < 256; ++b) {
-    keccak_f(s);
-    // 42 dwords = 14 triplets of 8 twelve-bit candidates
+  for (; r < limit; r += stride) {
+    const size_t inst = FIX ? (size_t)fix[r] : r;
+    const size_t hs = inst % C;
+    const int xy = (int)(inst / C);
+    if (!FIX && hs >= n) return;
+    uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
+    const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
+    KState s;
+    kzero(s);
 #pragma unroll
-    for (int t = 0; t < 14; ++t) {
-      uint32_t d[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int di = 3 * t + e;
-        d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
-      }
-      int c[8];
-      split12(d[0], d[1], d[2], c);
-      const int before = cnt;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        ring[cnt & 15] = (uint16_t)c[e];
-        cnt += c[e] < Q;
-      }
-      const int ch = before >> 3;
-      if ((cnt >> 3) != ch && ch < 32) {
-        const uint2 lo = *(const uint2*)(ring + (ch & 1) * 8);
-        const uint2 hi = *(const uint2*)(ring + (ch & 1) * 8 + 4);
-        dst[ch * 64] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      }
+    for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
+    s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
+    s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
+    int cnt = 0;
+#pragma unroll 1
+    for (int b = 0; b < (FIX ? MAX_XOF_BLOCKS : 3) && (!FIX || cnt < 256); ++b) {
+      keccak_f(s);
+      compact_block(s, ring, cnt, dst);
+    }
+    if (!FIX) {
+      if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
+      return;
     }
   }
 }
@@ -660,9 +680,10 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 // Scratch carve-up for a chunk of C handshakes
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
+  uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C;
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 2;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -678,6 +699,9 @@ inline ScratchView carve(void* base, int K, size_t C) {
   v.kprime = p;
   p += 4 * C;
   v.kbar = p;
+  p += 4 * C;
+  v.nfix = (uint32_t*)p;
+  v.fix = v.nfix + 2;
   return v;
 }
 
@@ -875,51 +899,85 @@ __global__ __launch_bounds__(256) void k_decrypt_core(size_t n, const uint8_t* _
 inline unsigned blocks_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
+// Two-stream schedule per chunk: the SampleNTT chain (k_xof, k_xof_fix) only
+// needs rho, so it runs on the side stream while the main stream does the
+// front hashes and PRFs; the core kernel joins both.  The fork is recorded
+// after the previous chunk's core, so reused scratch is never overwritten early.
+inline void fork(const Streams& s) {
+  if (!s.aux) return;
+  (void)hipEventRecord(s.fork, s.main);
+  (void)hipStreamWaitEvent(s.aux, s.fork, 0);
+}
+inline void join(const Streams& s) {
+  if (!s.aux) return;
+  (void)hipEventRecord(s.join, s.aux);
+  (void)hipStreamWaitEvent(s.main, s.join, 0);
+}
+
 template <int K>
-hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
+void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st) {
+  (void)hipMemsetAsync(v.nfix, 0, 4, st);
+  QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
+             C, (uint4*)v.xof, v.fix, v.nfix);
+  QRK_LAUNCH("k_xof_fix", st, (k_xof<K, true>), dim3(256), dim3(256), 0, st, rho, stride, n, C, (uint4*)v.xof, v.fix,
+             v.nfix);
+}
+
+template <int K>
+hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk, v.seeds);
-  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds, n,
-                     C, 2 * K, 2 * K, v.prf);
-  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
-                     (size_t)P<K>::PK, n, C, (uint4*)v.xof);
-  QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C, v.xof,
-                     v.prf, pk, sk);
+  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
+  QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
+             v.seeds);
+  fork(s);
+  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd);
+  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
+             n, C, 2 * K, 2 * K, v.prf);
+  join(s);
+  QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
+             n, C, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
 
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
-                       int32_t* status, void* scratch, hipStream_t st) {
+                       int32_t* status, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss, v.seeds);
+  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
+  fork(s);
+  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd);
+  QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
+             v.seeds);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-                     v.seeds, n, C, 2 * K + 1, K, v.prf);
-  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, pk + 384 * K,
-                     (size_t)P<K>::PK, n, C, (uint4*)v.xof);
-  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st, n, C,
-                     v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr, nullptr);
+             v.seeds, n, C, 2 * K + 1, K, v.prf);
+  join(s);
+  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256),
+             0, st, n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
+             nullptr);
   return hipGetLastError();
 }
 
 template <int K>
-hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch, hipStream_t st) {
+hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
+                       const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
+  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
+  fork(s);
+  launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n, v.seeds,
-                     v.kprime, v.kbar);
+  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
+             v.seeds, v.kprime, v.kbar);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-                     v.seeds, n, C, 2 * K + 1, K, v.prf);
-  QRK_LAUNCH("k_xof", st, k_xof<K>, dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, sk + 768 * K,
-                     (size_t)P<K>::SK, n, C, (uint4*)v.xof);
-  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf, sk + 384 * K,
-                     (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
-                     (int32_t*)nullptr, v.kprime, v.kbar, ss);
+             v.seeds, n, C, 2 * K + 1, K, v.prf);
+  join(s);
+  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf,
+             sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
+             (int32_t*)nullptr, v.kprime, v.kbar, ss);
   return hipGetLastError();
 }
 
@@ -930,7 +988,7 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
 }
 
 hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
-                         hipStream_t st) {
+                         const Streams& st) {
   if (n == 0) return hipSuccess;
   switch (a.k) {
     case 2: return mlkem::keygen_impl<2>(n, pk, sk, coins, scratch, st);
@@ -941,7 +999,7 @@ hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, c
 }
 
 hipError_t mlkem_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
-                        const uint8_t* coins, int32_t* status, void* scratch, hipStream_t st) {
+                        const uint8_t* coins, int32_t* status, void* scratch, const Streams& st) {
   if (n == 0) return hipSuccess;
   switch (a.k) {
     case 2: return mlkem::encaps_impl<2>(n, ct, ss, pk, coins, status, scratch, st);
@@ -952,7 +1010,7 @@ hipError_t mlkem_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, co
 }
 
 hipError_t mlkem_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
-                        void* scratch, hipStream_t st) {
+                        void* scratch, const Streams& st) {
   if (n == 0) return hipSuccess;
   switch (a.k) {
     case 2: return mlkem::decaps_impl<2>(n, ss, ct, sk, scratch, st);

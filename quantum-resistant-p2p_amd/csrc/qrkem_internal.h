@@ -51,21 +51,29 @@ struct Scratch {
 size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk);
 size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk);
 
+// Main stream (the caller's) plus an optional side stream and two events used
+// to fork/join independent kernel chains inside one operation.
+struct Streams {
+  hipStream_t main = nullptr;
+  hipStream_t aux = nullptr;  // nullptr: single-stream schedule
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
 // All pointers are device pointers; n handshakes processed as one chunk
 // (the caller splits large batches).  Return hipError_t.
 hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
-                         void* scratch, hipStream_t st);
+                         void* scratch, const Streams& st);
 hipError_t mlkem_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
-                        const uint8_t* coins, int32_t* status, void* scratch, hipStream_t st);
+                        const uint8_t* coins, int32_t* status, void* scratch, const Streams& st);
 hipError_t mlkem_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
-                        void* scratch, hipStream_t st);
+                        void* scratch, const Streams& st);
 
 hipError_t frodo_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
-                         void* scratch, hipStream_t st);
+                         void* scratch, const Streams& st);
 hipError_t frodo_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk,
-                        const uint8_t* coins, void* scratch, hipStream_t st);
+                        const uint8_t* coins, void* scratch, const Streams& st);
 hipError_t frodo_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
-                        void* scratch, hipStream_t st);
+                        void* scratch, const Streams& st);
 
 // SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len) for i < n, len <= 136.
 hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st);

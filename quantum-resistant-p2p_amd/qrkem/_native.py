@@ -41,6 +41,7 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_ctx_create": (ct.c_int, [ct.POINTER(P), ct.c_int]),
         "qrk_ctx_destroy": (None, [P]),
         "qrk_ctx_set_chunk": (ct.c_int, [P, SZ]),
+        "qrk_ctx_set_streams": (ct.c_int, [P, ct.c_int]),
         "qrk_ctx_scratch_bytes": (SZ, [P]),
         "qrk_kem_sizes": (ct.c_int, [ct.c_char_p, ct.POINTER(SZ)]),
         "qrk_kem_keypair_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P]),

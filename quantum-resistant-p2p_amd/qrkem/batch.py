@@ -161,6 +161,10 @@ class BatchKEM:
                     "decaps")
         return ss
 
+    def set_streams(self, streams: int) -> None:
+        """2: fork independent kernel chains onto a side stream (default); 1: serial."""
+        self._check(LIB.qrk_ctx_set_streams(self._ctx, streams), "set_streams")
+
     # ------------------------------------------------------------------ kernel timing
     def profile(self, enable: bool = True) -> None:
         """Reset and enable/disable per-kernel HIP-event timing on the launch stream."""

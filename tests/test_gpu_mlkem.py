@@ -146,3 +146,45 @@ def test_tamper_kernel_matches_definition(engines):
             bit = (h >> 1) % (8 * L)
             want[bit // 8] = 1 << (bit % 8)
         assert np.array_equal(got[i], want), i
+
+
+@pytest.mark.parametrize("alg", ALGS)
+def test_kat_drbg_records_match_golden(engines, golden_dir, alg):
+    """BASELINE.json configs[0] on the GPU: every NIST-KAT-DRBG record (1024 for
+    ML-KEM-768) byte-exact against the golden digests of the Python restatement."""
+    import json
+    import oracle as orc
+    g = json.loads((golden_dir / "kat_mlkem.json").read_text())[alg]
+    n = g["count"]
+    _, kc, ec = orc.kat_coins(n, 64, 32)
+    eng = engines[alg]
+    pk, sk = eng.keypair(coins=_dev(kc))
+    ct, ss = eng.encaps(pk, coins=_dev(ec))
+    ss2 = eng.decaps(sk, ct)
+    pk, sk, ct, ss, ss2 = map(_host, (pk, sk, ct, ss, ss2))
+    assert np.array_equal(ss, ss2)
+    for name, arr in (("pk", pk), ("sk", sk), ("ct", ct), ("ss", ss)):
+        assert hashlib.sha256(arr.tobytes()).hexdigest() == g["digests"][name], name
+
+
+def test_large_batch_roundtrip_and_sample(engines):
+    """2^16 handshakes (several chunks with a small chunk size): every ss_enc == ss_dec,
+    a stride sample byte-exact vs the oracle."""
+    import oracle as orc
+    from qrkem.batch import BatchKEM
+    alg, n = "ML-KEM-768", 1 << 16
+    eng = BatchKEM(alg, device=0, chunk=10000)
+    coins = eng.bench_coins(n, 96, seed=42)
+    kc, ec = coins[:, :64].contiguous(), coins[:, 64:].contiguous()
+    pk, sk = eng.keypair(coins=kc)
+    ct, ss = eng.encaps(pk, coins=ec)
+    ss2 = eng.decaps(sk, ct)
+    torch.cuda.synchronize()
+    assert bool((ss == ss2).all())
+    idx = np.r_[0:64, 9999:10003, 4096:n:4096, n - 5:n]
+    pk_h, sk_h, ct_h, ss_h = (t.cpu().numpy()[idx] for t in (pk, sk, ct, ss))
+    kc_h, ec_h = kc.cpu().numpy()[idx], ec.cpu().numpy()[idx]
+    opk, osk = orc.batch_keypair(alg, np.ascontiguousarray(kc_h))
+    oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h))
+    assert np.array_equal(pk_h, opk) and np.array_equal(sk_h, osk)
+    assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)

@@ -77,6 +77,36 @@ __global__ void k_mullo(uint32_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
+
+#define MKK(NAME, INSTR, INIT_B)                                                               \
+  __global__ void k_##NAME(uint32_t* out, uint32_t seed) {                                  \
+    uint32_t a0 = seed + threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 9,   \
+             a5 = a0 * 11, a6 = a0 * 13, a7 = a0 * 15, b = INIT_B;                          \
+    for (int i = 0; i < ITERS; ++i) {                                                        \
+      asm volatile(INSTR : "+v"(a0) : "v"(b)); asm volatile(INSTR : "+v"(a1) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a2) : "v"(b)); asm volatile(INSTR : "+v"(a3) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a4) : "v"(b)); asm volatile(INSTR : "+v"(a5) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a6) : "v"(b)); asm volatile(INSTR : "+v"(a7) : "v"(b));      \
+    }                                                                                        \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;    \
+  }
+MKK(mul_lo_u16, "v_mul_lo_u16 %0, %0, %1", seed | 1)
+MKK(mul_i32_i24, "v_mul_i32_i24 %0, %0, %1", seed & 0xFFF)
+MKK(mul_u32_u24, "v_mul_u32_u24 %0, %0, %1", seed & 0xFFF)
+MKK(mul_hi_u32_u24, "v_mul_hi_u32_u24 %0, %0, %1", seed & 0xFFF)
+MKK(mul_f32, "v_mul_f32 %0, %0, %1", 0x3f800001u)
+MKK(fma_f32, "v_fma_f32 %0, %0, %1, %1", 0x3f000000u)
+MKK(rndne_f32, "v_rndne_f32 %0, %0 ; %1", 0u)
+MKK(dot2c_i32_i16, "v_dot2c_i32_i16 %0, %1, %1", seed)
+MKK(bcnt, "v_bcnt_u32_b32 %0, %0, %1", seed)
+MKK(perm, "v_perm_b32 %0, %0, %1, %1", seed)
+MKK(bfe_u32, "v_bfe_u32 %0, %0, 3, 12 ; %1", seed)
+MKK(add_u32, "v_add_u32 %0, %0, %1", seed)
+MKK(lshl_add, "v_lshl_add_u32 %0, %0, 3, %1", seed)
+MKK(ashr, "v_ashrrev_i32 %0, 16, %0 ; %1", seed)
+MKK(pk_add_u16, "v_pk_add_u16 %0, %0, %1", seed)
+MKK(pk_mul_lo_u16, "v_pk_mul_lo_u16 %0, %0, %1", seed)
+
 // Keccak-f[1600] on register state, PERMS permutations per lane
 __global__ __launch_bounds__(256) void k_keccak(uint64_t* out, int perms) {
   qrk::KState s;
@@ -106,7 +136,11 @@ int main() {
     const char* name;
     void (*fn)(uint32_t*, uint32_t);
   } ks[] = {{"bitop3", k_bitop3}, {"alignbit", k_alignbit}, {"xor", k_xor}, {"mad_u32_u24", k_mad24},
-            {"mul_lo_u32", k_mullo}};
+            {"mul_lo_u32", k_mullo}, {"mul_lo_u16", k_mul_lo_u16}, {"mul_i32_i24", k_mul_i32_i24},
+            {"mul_u32_u24", k_mul_u32_u24}, {"mul_hi_u32_u24", k_mul_hi_u32_u24}, {"mul_f32", k_mul_f32},
+            {"fma_f32", k_fma_f32}, {"rndne_f32", k_rndne_f32}, {"dot2c_i32_i16", k_dot2c_i32_i16}, {"bcnt", k_bcnt},
+            {"perm", k_perm}, {"bfe_u32", k_bfe_u32}, {"add_u32", k_add_u32}, {"lshl_add", k_lshl_add}, {"ashr", k_ashr},
+            {"pk_add_u16", k_pk_add_u16}, {"pk_mul_lo_u16", k_pk_mul_lo_u16}};
   for (auto& k : ks) {
     hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(threads), 0, 0, d, 1u);
     CHECK(hipDeviceSynchronize());
