@@ -162,7 +162,8 @@ def main():
     alg = args.alg
     B = 1 << args.log2_batch
     eng = BatchKEM(alg, device=local, chunk=args.chunk)
-    base = rank * B  # global index range [base, base + B)
+    from qrkem.shard import reduce_run, weak_shard
+    base = weak_shard(rank, world, B).first  # global index range [base, base + B)
 
     coins = eng.bench_coins(B, 96, args.seed, base)
     kc = coins[:, :64].contiguous()
@@ -219,13 +220,7 @@ def main():
 
     ct, ss, ss2 = out
     mismatches = int((ss != ss2).any(dim=1).sum().item()) if args.mode == "encdec" else 0
-    t = torch.tensor([elapsed, float(mismatches)], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        tm = t[:1].clone()
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        cnt = t[1:].clone()
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        elapsed, mismatches = float(tm.item()), int(cnt.item())
+    elapsed, (mismatches,) = reduce_run(elapsed, [mismatches], device=f"cuda:{local}")
 
     total = B * world * args.steps
     value = total / elapsed

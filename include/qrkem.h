@@ -81,6 +81,21 @@ OQS_STATUS OQS_KEM_keypair_derand(const OQS_KEM *kem, uint8_t *public_key, uint8
 OQS_STATUS OQS_KEM_encaps_derand(const OQS_KEM *kem, uint8_t *ciphertext, uint8_t *shared_secret,
                                  const uint8_t *public_key, const uint8_t *seed);
 
+/* Signature half of the liboqs ABI: the reference's oqs.py binds these at
+ * import time (oqs.py:684-697).  Signatures are outside this engine's scope,
+ * so the registry is empty (count 0) and every call fails. */
+typedef struct OQS_SIG OQS_SIG;
+size_t OQS_SIG_alg_count(void);
+const char *OQS_SIG_alg_identifier(size_t i);
+int OQS_SIG_alg_is_enabled(const char *method_name);
+OQS_SIG *OQS_SIG_new(const char *method_name);
+OQS_STATUS OQS_SIG_keypair(const OQS_SIG *sig, uint8_t *public_key, uint8_t *secret_key);
+OQS_STATUS OQS_SIG_sign(const OQS_SIG *sig, uint8_t *signature, size_t *signature_len, const uint8_t *message,
+                        size_t message_len, const uint8_t *secret_key);
+OQS_STATUS OQS_SIG_verify(const OQS_SIG *sig, const uint8_t *message, size_t message_len,
+                          const uint8_t *signature, size_t signature_len, const uint8_t *public_key);
+void OQS_SIG_free(OQS_SIG *sig);
+
 /* ------------------------------------------------------------------ *
  * Part 2: batched device API (no reference equivalent)                *
  * ------------------------------------------------------------------ */

@@ -430,6 +430,23 @@ OQS_STATUS OQS_KEM_decaps(const OQS_KEM* kem, uint8_t* ss, const uint8_t* ct, co
 }
 void OQS_KEM_free(OQS_KEM* kem) { free(kem); }
 
+// Empty signature registry (see include/qrkem.h)
+size_t OQS_SIG_alg_count(void) { return 0; }
+const char* OQS_SIG_alg_identifier(size_t) { return nullptr; }
+int OQS_SIG_alg_is_enabled(const char*) { return 0; }
+OQS_SIG* OQS_SIG_new(const char*) {
+  fail("signatures are not implemented by libqrkem");
+  return nullptr;
+}
+OQS_STATUS OQS_SIG_keypair(const OQS_SIG*, uint8_t*, uint8_t*) { return OQS_ERROR; }
+OQS_STATUS OQS_SIG_sign(const OQS_SIG*, uint8_t*, size_t*, const uint8_t*, size_t, const uint8_t*) {
+  return OQS_ERROR;
+}
+OQS_STATUS OQS_SIG_verify(const OQS_SIG*, const uint8_t*, size_t, const uint8_t*, size_t, const uint8_t*) {
+  return OQS_ERROR;
+}
+void OQS_SIG_free(OQS_SIG*) {}
+
 void OQS_MEM_cleanse(void* ptr, size_t len) {
   if (!ptr) return;
   volatile uint8_t* p = (volatile uint8_t*)ptr;
