@@ -27,11 +27,11 @@ static AlgInfo ALGS[] = {
     {"ML-KEM-768", Family::MLKEM, 3, 3, 1184, 2400, 1088, 32, 64, 32, false, true},
     {"ML-KEM-1024", Family::MLKEM, 5, 4, 1568, 3168, 1568, 32, 64, 32, false, true},
     {"FrodoKEM-640-AES", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, true, false},
-    {"FrodoKEM-640-SHAKE", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, false, false},
+    {"FrodoKEM-640-SHAKE", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, false, true},
     {"FrodoKEM-976-AES", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, true, false},
-    {"FrodoKEM-976-SHAKE", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, false, false},
+    {"FrodoKEM-976-SHAKE", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, false, true},
     {"FrodoKEM-1344-AES", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, true, false},
-    {"FrodoKEM-1344-SHAKE", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, false, false},
+    {"FrodoKEM-1344-SHAKE", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, false, true},
 };
 static const int NALG = (int)(sizeof(ALGS) / sizeof(ALGS[0]));
 
@@ -198,7 +198,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
                      const uint8_t* i2, int32_t* status, hipStream_t st) {
   if (n == 0) return 0;
   if (ensure_device(ctx->device)) return -1;
-  const size_t chunk = std::min(ctx->chunk, n);
+  // FrodoKEM scratch is ~50-100 KB per handshake: cap its chunk at 2^14
+  const size_t cap = a.family == Family::FRODO ? std::min<size_t>(ctx->chunk, 16384) : ctx->chunk;
+  const size_t chunk = std::min(cap, n);
   if (grow_device(&ctx->scratch, &ctx->scratch_bytes, scratch_for(a, chunk), st)) return -1;
   // coins: NULL -> OS CSPRNG, uploaded to device staging
   const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
@@ -252,8 +254,11 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
           e = frodo_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, S);
           break;
         case Op::ENCAPS:
-          e = frodo_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
-                           ctx->scratch, S);
+          // FrodoKEM encapsulation has no public-key validity check: status is always 0
+          if (status) e = hipMemsetAsync(status + off, 0, m * sizeof(int32_t), st);
+          if (e == hipSuccess)
+            e = frodo_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen,
+                             ctx->scratch, S);
           break;
         case Op::DECAPS:
           e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);

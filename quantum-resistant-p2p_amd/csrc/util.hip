@@ -68,20 +68,4 @@ hipError_t tamper_ciphertexts(size_t n, size_t ctlen, uint64_t seed, int mode, u
   return hipGetLastError();
 }
 
-// FrodoKEM: HIP implementation lands in frodo.hip; until then the algorithms are
-// listed as supported-but-not-enabled (OQS_KEM_alg_is_enabled == 0).
-__attribute__((weak)) size_t frodo_scratch_bytes(const AlgInfo&, size_t) { return 0; }
-__attribute__((weak)) hipError_t frodo_keypair(const AlgInfo&, size_t, uint8_t*, uint8_t*, const uint8_t*, void*,
-                                               const Streams&) {
-  return hipErrorNotSupported;
-}
-__attribute__((weak)) hipError_t frodo_encaps(const AlgInfo&, size_t, uint8_t*, uint8_t*, const uint8_t*,
-                                              const uint8_t*, void*, const Streams&) {
-  return hipErrorNotSupported;
-}
-__attribute__((weak)) hipError_t frodo_decaps(const AlgInfo&, size_t, uint8_t*, const uint8_t*, const uint8_t*,
-                                              void*, const Streams&) {
-  return hipErrorNotSupported;
-}
-
 }  // namespace qrk
