@@ -44,8 +44,8 @@ def mlkem_sizes(alg):
     return 384 * k + 32, 768 * k + 96, 32 * (du * k + dv)
 
 
-def perms_encdec(alg) -> int:
-    """FIPS-minimal Keccak permutations per Encaps + Decaps (SampleNTT at 3 blocks)."""
+def mlkem_perms(alg):
+    """FIPS-minimal Keccak permutations per Encaps and per Decaps (SampleNTT at 3 blocks)."""
     k, eta1, eta2, _, _ = KP[alg]
     pk, _, ct = mlkem_sizes(alg)
     h_ek = (pk + 1 + 135) // 136          # H(ek)      SHA3-256
@@ -53,31 +53,82 @@ def perms_encdec(alg) -> int:
     prf = k * (1 if eta1 == 2 else 2) + (k + 1)
     xof = 3 * k * k
     j = (32 + ct + 1 + 135) // 136         # J(z || c)  SHAKE256
-    enc = h_ek + g + prf + xof
-    dec = g + prf + xof + j
+    return h_ek + g + prf + xof, g + prf + xof + j
+
+
+def perms_encdec(alg) -> int:
+    enc, dec = mlkem_perms(alg)
     return enc + dec
 
 
-def valu_ops_encdec(alg) -> int:
-    """W = P*4320 + (NTT + NTT^-1)*896*8 + basemul_polys*3584."""
+def valu_ops(alg, mode="encdec") -> int:
+    """W = P*4320 + (NTT + NTT^-1)*896*8 + basemul_polys*3584 per Encaps+Decaps
+    (mode "encdec") or per Decaps (mode "decaps-tampered").  FrodoKEM: P*4320 (the S'A
+    contraction runs on MFMA and is priced separately)."""
+    if alg in FP:
+        p = frodo_perms(alg)
+        enc = p["k_fr_front_enc"] + p["k_fr_gen_at"] + p["k_fr_se_stream"] + p["k_fr_ss"]
+        dec = p["k_fr_g2_dec"] + p["k_fr_gen_at"] + p["k_fr_se_stream"] + p["k_fr_ss"]
+        return (enc + dec if mode == "encdec" else dec) * PERM_OPS
     k = KP[alg][0]
-    ntts = (k + (k + 1)) + (k + 1) + (k + (k + 1))  # enc: k fwd, k+1 inv; dec: k fwd + 1 inv; re-enc
-    basemul_polys = (k * k + k) + k + (k * k + k)
-    return perms_encdec(alg) * PERM_OPS + ntts * 896 * 8 + basemul_polys * 3584
+    enc_p, dec_p = mlkem_perms(alg)
+    enc = enc_p * PERM_OPS + (k + (k + 1)) * 896 * 8 + (k * k + k) * 3584
+    dec = dec_p * PERM_OPS + ((k + 1) + (k + (k + 1))) * 896 * 8 + (k + (k * k + k)) * 3584
+    return enc + dec if mode == "encdec" else dec
 
 
-def kernel_ops_per_instance(alg, name):
-    """Algorithmic VALU ops of one lane-instance of a Keccak-stage kernel (launch = instances x this)."""
+def valu_ops_encdec(alg) -> int:
+    return valu_ops(alg, "encdec")
+
+
+# FrodoKEM (n, logq, sec, hash rate bytes): FrodoKEM spec round 3 / SURVEY.md 8a A18-A21
+FP = {"FrodoKEM-640-SHAKE": (640, 15, 16, 168), "FrodoKEM-976-SHAKE": (976, 16, 24, 136),
+      "FrodoKEM-1344-SHAKE": (1344, 16, 32, 136)}
+MFMA_I8_PEAK = 5.0e15  # dense int8 MFMA ops/s (MI355X_MICROARCH.md: I8 = 2x BF16 per clock, BF16 ~2.5 PF dense)
+
+
+def frodo_sizes(alg):
+    n, logq, sec, _ = FP[alg]
+    pk = 16 + logq * n
+    return pk, sec + pk + 16 * n + sec, logq * n + 8 * logq
+
+
+def frodo_perms(alg):
+    """Keccak permutations per Encaps / per Decaps, by kernel (FIPS-minimal sponge counts)."""
+    n, logq, sec, rate = FP[alg]
+    pk, _, ct = frodo_sizes(alg)
+    se_words = (2 * n + 8) * 8 * 2 // 8
+    gen_a = n * -(-2 * n // 168)                       # SHAKE128 rows of A
+    se = -(-se_words * 8 // rate)                      # SHAKE(0x96 || seedSE) stream
+    ss = -(-(ct + sec + 1) // rate)                    # ss = H(ct || k)
+    return {"k_fr_gen_at": gen_a, "k_fr_se_stream": se, "k_fr_ss": ss,
+            "k_fr_front_enc": -(-(pk + 1) // rate) + 1, "k_fr_g2_dec": 1}
+
+
+def kernel_ops_per_hs(alg, name, mode):
+    """Algorithmic ops one handshake contributes to kernel `name` in one bench step
+    (encaps+decaps, or decaps only) and the bound they are priced against."""
+    calls = 2 if mode == "encdec" else 1  # kernels shared by Encaps and Decaps run once per op
+    if alg in FP:
+        n = FP[alg][0]
+        if name == "k_fr_mm":  # S'A: 8 x n x n MACs on two int8 limbs, 2 ops per MAC
+            return calls * 2 * 2 * 8 * n * n, "mfma"
+        perms = frodo_perms(alg)
+        if name in ("k_fr_front_enc",):
+            return (perms[name] * PERM_OPS if mode == "encdec" else None), "valu"
+        if name in perms:
+            return calls * perms[name] * PERM_OPS, "valu"
+        return None, None
     k, eta1, _, _, _ = KP[alg]
     pk, _, ct = mlkem_sizes(alg)
     if name == "k_xof":
-        return 3 * PERM_OPS, k * k
-    if name == "k_front_encaps":
-        return ((pk + 1 + 135) // 136 + 1) * PERM_OPS, 1
+        return calls * 3 * k * k * PERM_OPS, "valu"
+    if name == "k_front_encaps" and mode == "encdec":
+        return ((pk + 1 + 135) // 136 + 1) * PERM_OPS, "valu"
     if name == "k_front_decaps":
-        return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, 1
+        return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
     if name == "k_prf":
-        return ((k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS) / (2 * k + 1), 2 * k + 1
+        return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
     return None, None
 
 
@@ -93,9 +144,11 @@ def cpu_threads() -> int:
     return max(1, min(n, cap, 16))
 
 
-def cpu_baseline(alg, pk, sk, ec, ct_gpu, ss_gpu, B):
-    """Oracle (C restatement, 'port') timed on host cores over a bounded sample; also checks
-    the GPU outputs for the sampled indices byte-for-byte."""
+def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
+    """Oracle (C restatement, 'port') timed on host cores over a bounded sample (~12 s);
+    also checks the GPU outputs for the sampled indices byte-for-byte.
+    mode "encdec": Encaps(pk, ec) + Decaps; ct_in / ss_gpu = the GPU's ct / ss.
+    mode "decaps-tampered": Decaps(sk, ct_in) only; ss_gpu = the GPU's ss."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as orc
     threads = cpu_threads()
@@ -103,36 +156,87 @@ def cpu_baseline(alg, pk, sk, ec, ct_gpu, ss_gpu, B):
     def take(t, n):
         return np.ascontiguousarray(t[:n].cpu().numpy())
 
-    cal = min(1024, B)
-    pk_c, sk_c, ec_c = take(pk, cal), take(sk, cal), take(ec, cal)
+    def run(n):
+        if mode == "encdec":
+            c, s = orc.batch_encaps(alg, take(pk, n), take(ec, n), threads)
+            return c, s, orc.batch_decaps(alg, take(sk, n), c, threads)
+        return None, None, orc.batch_decaps(alg, take(sk, n), take(ct_in, n), threads)
+
+    cal = min(256 if alg in FP else 1024, B)
     t0 = time.perf_counter()
-    c, s = orc.batch_encaps(alg, pk_c, ec_c, threads)
-    orc.batch_decaps(alg, sk_c, c, threads)
+    run(cal)
     rate = cal / max(time.perf_counter() - t0, 1e-6)
-    S = int(min(B, max(cal, (rate * 12.0) // 1024 * 1024)))
-    pk_s, sk_s, ec_s = take(pk, S), take(sk, S), take(ec, S)
+    S = int(min(B, max(cal, (rate * 12.0) // 256 * 256)))
+    sk_s = take(sk, S)
     t0 = time.perf_counter()
-    c, s = orc.batch_encaps(alg, pk_s, ec_s, threads)
-    s2 = orc.batch_decaps(alg, sk_s, c, threads)
+    c, s, s2 = run(S)
     dt = time.perf_counter() - t0
-    match = bool(np.array_equal(c, take(ct_gpu, S)) and np.array_equal(s, take(ss_gpu, S))
-                 and np.array_equal(s2, s))
+    if mode == "encdec":
+        match = bool(np.array_equal(c, take(ct_in, S)) and np.array_equal(s, take(ss_gpu, S))
+                     and np.array_equal(s2, s))
+    else:
+        match = bool(np.array_equal(s2, take(ss_gpu, S)))
     # the reference call pattern: one handshake per Python call, one core
+    pk_s, ec_s, ct_s = take(pk, S), take(ec, S), take(ct_in, S)
     t0 = time.perf_counter()
     m = 0
     while time.perf_counter() - t0 < 2.0 and m < S:
-        cc, ss_ = orc.encaps(alg, pk_s[m].tobytes(), ec_s[m].tobytes())
+        if mode == "encdec":
+            cc, _ = orc.encaps(alg, pk_s[m].tobytes(), ec_s[m].tobytes())
+        else:
+            cc = ct_s[m].tobytes()
         orc.decaps(alg, sk_s[m].tobytes(), cc)
         m += 1
     single = m / (time.perf_counter() - t0)
+    spec = "FrodoKEM round 3" if alg in FP else "FIPS 203"
     return {
-        "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port",
+        "value": S / dt, "unit": "encaps+decaps/s" if mode == "encdec" else "decaps/s", "cores": threads,
+        "kind": "port",
         "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so, C restatement of "
-                  f"FIPS 203, -O3 -march=native, {threads} pthreads); liboqs itself is absent "
+                  f"{spec}, -O3 -march=native, {threads} pthreads); liboqs itself is absent "
                   f"(.MISSING_LARGE_BLOBS:1)",
         "sample_matches_gpu": match,
         "single_core_python_per_call": single,
     }
+
+
+def kernel_report(alg, mode, prof, B):
+    """Per-kernel algorithmic rate from the serial profiled step: ops per handshake x B / total
+    kernel time.  Returns (kernels, roofline-of-dominant, mfma-object-or-None)."""
+    kernels = {}
+    tot_ms = sum(ms for ms, _ in prof.values()) or 1.0
+    for name, (ms, cnt) in prof.items():
+        ops, bound = kernel_ops_per_hs(alg, name, mode)
+        kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot_ms}
+        if ops is not None:
+            rate = ops * B / (ms * 1e-3)
+            peak = MFMA_I8_PEAK if bound == "mfma" else VALU_PEAK
+            kernels[name].update(bound=bound, achieved_Tops=rate / 1e12, frac=rate / peak)
+    roof, mfma = None, None
+    if prof:
+        dom = max(prof, key=lambda k: prof[k][0])
+        ops, bound = kernel_ops_per_hs(alg, dom, mode)
+        ms, cnt = prof[dom]
+        if ops is not None:
+            achieved = ops * B / (ms * 1e-3)
+            peak = MFMA_I8_PEAK if bound == "mfma" else VALU_PEAK
+            roof = {"kernel": dom, "bound": bound, "achieved": achieved / 1e12, "peak": peak / 1e12,
+                    "unit": "Top/s (int32 lane-ops)" if bound == "valu" else "Top/s (int8 MFMA ops)",
+                    "frac": achieved / peak, "traffic": None,
+                    "ops_per_launch": ops * B / cnt, "avg_launch_ms": ms / cnt}
+        if "k_fr_mm" in prof:
+            n = FP[alg][0]
+            np_ = -(-n // 128) * 128
+            calls = 2 if mode == "encdec" else 1
+            ms, cnt = prof["k_fr_mm"]
+            alg_ops = calls * 2 * 2 * 8 * n * n * B
+            issued = calls * 2 * (16 * 16 * 64 * 2) * (np_ // 64) * (n // 16) * B
+            mfma = {"kernel": "k_fr_mm", "achieved": alg_ops / (ms * 1e-3) / 1e12,
+                    "issued": issued / (ms * 1e-3) / 1e12, "peak": MFMA_I8_PEAK / 1e12,
+                    "unit": "Top/s (int8 MFMA ops; algorithmic = 2 limbs x 2 x 8 x n^2 per S'A)",
+                    "frac": alg_ops / (ms * 1e-3) / MFMA_I8_PEAK, "share_of_step_kernels": ms / tot_ms,
+                    "avg_launch_ms": ms / cnt}
+    return kernels, roof, mfma
 
 
 def main():
@@ -141,7 +245,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--alg", default="ML-KEM-768")
-    ap.add_argument("--log2-batch", type=int, default=20)
+    ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM)")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered"], default="encdec")
@@ -159,15 +263,19 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from qrkem.batch import BatchKEM
-    alg = args.alg
-    B = 1 << args.log2_batch
-    eng = BatchKEM(alg, device=local, chunk=args.chunk)
     from qrkem.shard import reduce_run, weak_shard
+    alg = args.alg
+    frodo = alg in FP
+    lb = args.log2_batch if args.log2_batch is not None else (16 if frodo else 20)
+    B = 1 << lb
+    eng = BatchKEM(alg, device=local, chunk=args.chunk)
+    chunk_eff = min(args.chunk, B, 16384) if frodo else min(args.chunk, B)
     base = weak_shard(rank, world, B).first  # global index range [base, base + B)
 
-    coins = eng.bench_coins(B, 96, args.seed, base)
-    kc = coins[:, :64].contiguous()
-    ec = coins[:, 64:].contiguous()
+    kpl, encl = eng.kp_coins, eng.enc_coins
+    coins = eng.bench_coins(B, kpl + encl, args.seed, base)
+    kc = coins[:, :kpl].contiguous()
+    ec = coins[:, kpl:].contiguous()
     del coins
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -179,31 +287,44 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def timed(step):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        barrier()
+        return time.perf_counter() - t0, out
+
+    checks = {}
+    variants = {}
     if args.mode == "encdec":
         def step():
             ct_, ss_ = eng.encaps(pk, coins=ec)
-            ss2_ = eng.decaps(sk, ct_)
-            return ct_, ss_, ss2_
+            return ct_, ss_, eng.decaps(sk, ct_)
+        main_step = step
     else:
-        ct0, ss0 = eng.encaps(pk, coins=ec)
-        eng.tamper(ct0, args.seed, 2)
+        ct_valid, ss0 = eng.encaps(pk, coins=ec)
+        cts = {"all-valid": ct_valid}
+        for name, m in (("all-tampered", 1), ("mixed", 2)):
+            c = ct_valid.clone()
+            eng.tamper(c, args.seed, m)
+            cts[name] = c
+        torch.cuda.synchronize()
+        for name in ("all-valid", "all-tampered"):
+            el, _ = timed(lambda c=cts[name]: eng.decaps(sk, c))
+            variants[name] = el * 1e3 / args.steps
 
-        def step():
-            return ct0, ss0, eng.decaps(sk, ct0)
+        def main_step():
+            return cts["mixed"], ss0, eng.decaps(sk, cts["mixed"])
 
-    for _ in range(args.warmup):
-        out = step()
-    torch.cuda.synchronize()
     if not args.no_profile:
         eng.profile(True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, out = timed(main_step)
     prof_live = eng.profile_read() if not args.no_profile else {}
     eng.profile(False)
     # Kernel-in-isolation pass (serial schedule, one untimed step): the forked
@@ -212,44 +333,44 @@ def main():
     if not args.no_profile:
         eng.set_streams(1)
         eng.profile(True)
-        step()
+        main_step()
         torch.cuda.synchronize()
-        prof = {k: (ms, cnt) for k, (ms, cnt) in eng.profile_read().items()}
+        prof = dict(eng.profile_read().items())
         eng.profile(False)
         eng.set_streams(2)
 
     ct, ss, ss2 = out
-    mismatches = int((ss != ss2).any(dim=1).sum().item()) if args.mode == "encdec" else 0
-    elapsed, (mismatches,) = reduce_run(elapsed, [mismatches], device=f"cuda:{local}")
+    if args.mode == "encdec":
+        bad = int((ss != ss2).any(dim=1).sum().item())
+        counters = [bad, 0]
+    else:
+        variants["mixed"] = elapsed * 1e3 / args.steps
+        tampered = (ct != cts["all-valid"]).any(dim=1)
+        same = (ss2 == ss).all(dim=1)
+        # valid rows must give the encapsulated key, tampered rows the implicit-rejection key
+        bad = int((same != ~tampered).sum().item())
+        counters = [bad, int(tampered.sum().item())]
+    elapsed, (bad, n_tampered) = reduce_run(elapsed, counters, device=f"cuda:{local}")
+    if args.mode == "encdec":
+        checks["ss_enc_eq_ss_dec_mismatches"] = bad
+    else:
+        checks["implicit_rejection_mismatches"] = bad
+        checks["tampered"] = n_tampered
+        checks["decaps_ms_per_step"] = variants
+        checks["tampered_over_valid_time"] = variants["all-tampered"] / variants["all-valid"]
 
     total = B * world * args.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
+    kernels, roof, mfma = kernel_report(alg, args.mode, prof, B)
 
-    # ---------------- roofline of the dominant kernel (live HIP events on the launch stream)
-    roof = None
-    kernels = {}
-    for name, (ms, cnt) in prof.items():
-        kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": None}
-    tot_ms = sum(ms for ms, _ in prof.values()) or 1.0
-    for name, (ms, _) in prof.items():
-        kernels[name]["share"] = ms / tot_ms
-    if prof:
-        dom = max(prof, key=lambda k: prof[k][0])
-        per_inst, inst_per_hs = kernel_ops_per_instance(alg, dom)
-        ms, cnt = prof[dom]
-        chunk = min(args.chunk, B)
-        if per_inst is not None:
-            ops_per_launch = per_inst * inst_per_hs * chunk
-            achieved = ops_per_launch / (ms / cnt * 1e-3)
-            roof = {"kernel": dom, "bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK / 1e12,
-                    "unit": "Top/s (int32 lane-ops)", "frac": achieved / VALU_PEAK, "traffic": None,
-                    "ops_per_launch": ops_per_launch, "avg_launch_ms": ms / cnt}
-
-    W = valu_ops_encdec(alg) if args.mode == "encdec" else None
+    W = valu_ops(alg, args.mode)
+    headline = alg == "ML-KEM-768" and args.mode == "encdec"
+    cfg_idx = 1 if not frodo and args.mode == "encdec" else (3 if frodo else 4)
+    what = "Encaps+Decaps" if args.mode == "encdec" else "Decaps, 50% tampered (mixed)"
     result = {
-        "metric": METRIC if (alg == "ML-KEM-768" and args.mode == "encdec")
-        else f"{alg} {args.mode} /sec at batch 2^{args.log2_batch} per GPU",
+        "metric": METRIC if headline else f"{alg} {'encaps+decaps' if args.mode == 'encdec' else 'decaps'}"
+                                          f"/sec at batch 2^{lb} per GPU",
         "value": value,
         "unit": "encaps+decaps/s" if args.mode == "encdec" else "decaps/s",
         "n_gpus": world,
@@ -259,24 +380,25 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32",
+        "dtype": "u32" if not frodo else "u32 (Keccak) + i8->i32 (MFMA)",
         "data": "synthetic: coins = SHAKE256('qrk-bench'||LE64(seed)||LE64(i)) generated on device; "
                 "keys from batched KeyGen on those coins",
-        "config": {"workload": f"{alg} {'Encaps+Decaps' if args.mode == 'encdec' else 'Decaps, 50% tampered'}"
-                               f" of 2^{args.log2_batch} device-resident handshakes per GPU (BASELINE.json configs[1])",
-                   "alg": alg, "batch_per_gpu": B, "global_batch": B * world, "chunk": min(args.chunk, B),
+        "config": {"workload": f"{alg} {what} of 2^{lb} device-resident handshakes per GPU "
+                               f"(BASELINE.json configs[{cfg_idx}])",
+                   "alg": alg, "batch_per_gpu": B, "global_batch": B * world, "chunk": chunk_eff,
                    "parallelism": f"index-sharded x{world} (no data-path collective)"},
         "roofline": roof,
-        "valu_frac_of_peak_step": (value * W / VALU_PEAK) if W else None,
-        "valu_ops_per_handshake": W,
+        "mfma": mfma,
+        "valu_frac_of_peak_step": value * W / VALU_PEAK,
+        "valu_ops_per_unit": W,
         "keygen_per_s": B * world / keygen_s if keygen_s > 0 else None,
         "kernels": kernels,
         "kernels_timed_region_forked": {k: {"avg_ms": ms / c, "launches": c} for k, (ms, c) in prof_live.items()},
-        "checks": {"ss_enc_eq_ss_dec_mismatches": mismatches if args.mode == "encdec" else None},
+        "checks": checks,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "encdec":
-        result["cpu_baseline"] = cpu_baseline(alg, pk, sk, ec, ct, ss, B)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(alg, args.mode, pk, sk, ec, ct, ss2 if args.mode != "encdec" else ss, B)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
