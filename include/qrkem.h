@@ -108,6 +108,9 @@ void qrk_ctx_destroy(qrk_ctx *ctx);
 /* Handshakes per internal chunk (scratch = chunk * per-handshake bytes). */
 int qrk_ctx_set_chunk(qrk_ctx *ctx, size_t chunk);
 size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
+/* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
+ * scratch stays near 8 GiB); 0 for an unknown algorithm. */
+size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
 /* 2 (default): independent kernel chains of one operation run forked on a
  * side stream and join the caller's stream; 1: everything on the caller's
  * stream (kernel timings in isolation). */

@@ -193,14 +193,25 @@ static const AlgInfo* resolve(const char* alg) {
 
 enum class Op { KEYPAIR, ENCAPS, DECAPS };
 
+// FrodoKEM scratch is 0.14-0.53 MB per handshake: its chunk is capped so scratch stays near 8 GiB
+static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
+  size_t cap = ctx->chunk;
+  if (a.family == Family::FRODO) {
+    const size_t per_hs = frodo_scratch_bytes(a, 1024) / 1024 + 1;
+    cap = std::min(cap, std::max<size_t>(4096, ((size_t)8 << 30) / per_hs / 64 * 64));
+  }
+  return cap;
+}
+
 // Core batched driver over device pointers, chunked.
 static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
                      const uint8_t* i2, int32_t* status, hipStream_t st) {
   if (n == 0) return 0;
   if (ensure_device(ctx->device)) return -1;
-  // FrodoKEM scratch is ~50-100 KB per handshake: cap its chunk at 2^14
-  const size_t cap = a.family == Family::FRODO ? std::min<size_t>(ctx->chunk, 16384) : ctx->chunk;
-  const size_t chunk = std::min(cap, n);
+  // equal chunks (multiples of 64) rather than full chunks plus a small tail
+  const size_t cap = chunk_for(ctx, a);
+  const size_t nchunks = (n + cap - 1) / cap;
+  const size_t chunk = std::min(cap, ((n + nchunks - 1) / nchunks + 63) & ~(size_t)63);
   if (grow_device(&ctx->scratch, &ctx->scratch_bytes, scratch_for(a, chunk), st)) return -1;
   // coins: NULL -> OS CSPRNG, uploaded to device staging
   const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
@@ -498,6 +509,11 @@ int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {
 }
 
 size_t qrk_ctx_scratch_bytes(const qrk_ctx* ctx) { return ctx ? ctx->scratch_bytes : 0; }
+
+size_t qrk_ctx_effective_chunk(const qrk_ctx* ctx, const char* alg) {
+  const AlgInfo* a = find_alg(alg);
+  return (ctx && a) ? chunk_for(ctx, *a) : 0;
+}
 
 int qrk_ctx_profile(qrk_ctx* ctx, int enable) {
   if (!ctx) return fail("null context");

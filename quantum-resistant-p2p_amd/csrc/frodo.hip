@@ -9,16 +9,18 @@
 // permutations; S'A = 3.3 M multiply-adds mod 2^16.  Kernels:
 //
 //   k_fr_front_enc    lane / hs   pkh = H(pk); (seedSE || k) = H(pkh || mu)
-//   k_fr_dec_m        wave / hs   M = C - B'S, mu' = Decode(M)               (VALU)
+//   k_fr_dec_m        256 / hs    M = C - B'S (B', S^T staged in LDS), mu' = Decode(M)
 //   k_fr_g2_dec       lane / hs   (seedSE' || k') = H(pkh || mu')
 //   k_fr_se_stream    lane / hs   SHAKE(0x96 || seedSE) raw words (123 perms, sequential)
 //   k_fr_sample       thread / 4 words   CDF sampler -> S' (int8, zero-padded), E', E''
-//   k_fr_gen_at       lane / row  Gen(A) row r -> balanced int8 limbs, written as
-//                                  transposed byte planes T[c][r] via an LDS stage
-//   k_fr_mm           wave / 16 cols    B' = S'A + E' on v_mfma_i32_16x16x64_i8:
-//                                  A = 256*hi + lo (balanced int8 limbs), two i8 MFMAs per
-//                                  K-step, int32 accumulation -> exact mod 2^16
-//   k_fr_pack         wave / hs   V = S'B + E'', C = V + Encode(mu), Pack(B', C);
+//   k_fr_gen_mm       wave / 64 rows   Gen(A) (lane = row, SHAKE128) fused with S'A on
+//                                  v_mfma_i32_16x16x64_i8: each squeezed block's 84 columns
+//                                  are split into balanced int8 limbs (A = 256*hi + lo) in
+//                                  LDS and contracted over the wave's 64 rows (two i8 MFMAs
+//                                  per 16 columns, int32 accumulation, exact mod 2^16);
+//                                  per-wave u16 partial sums of S'A go to scratch
+//   k_fr_pack         256 / hs    B' = sum(partials) + E', V = S'B + E'', C = V + Encode(mu),
+//                                  Pack(B', C) staged in LDS; encaps: coalesced ct store;
 //                                  decaps: compare with ct, select k' or s (constant time)
 //   k_fr_ss           lane / hs   ss = H(ct || k)
 // KeyGen: k_fr_kg_front (seedA, SHAKE(0x5F || seedSE) stream), k_fr_sample,
@@ -32,7 +34,7 @@ namespace frodo {
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int NBAR = 8;
-constexpr int SUB = 256;  // handshakes per Gen(A) / MFMA sub-chunk (A planes stay in the 256 MiB MALL for n = 640)
+constexpr int ST_PITCH = 72;  // LDS pitch (u16) of one column of a 64-row A block: 144 B -> conflict-free 16-B reads
 
 template <int N_>
 struct FP {
@@ -46,7 +48,8 @@ struct FP {
   static constexpr int CT = LOGQ * N + LOGQ * NBAR;
   static constexpr int SK = SEC + PK + 2 * N * NBAR + SEC;
   static constexpr int MU = EB * NBAR;  // bytes
-  static constexpr int NP = (N + 127) / 128 * 128;  // padded row pitch of S' / A planes
+  static constexpr int NP = (N + 127) / 128 * 128;  // padded row pitch of S' (>= 64 * NWV, zero padded)
+  static constexpr int NWV = (N + 63) / 64;         // 64-row waves of Gen(A) per handshake
   static constexpr int SE_WORDS = (2 * N + NBAR) * NBAR * 2 / 8;  // encaps sampler stream (u64)
   static constexpr int KG_WORDS = 2 * N * NBAR * 2 / 8;           // keygen sampler stream (u64)
   static constexpr int A_BLOCKS = (2 * N + 167) / 168;            // SHAKE128 blocks per row of A
@@ -84,11 +87,9 @@ struct View {
   int8_t* sp8;     // S' (or S^T for KeyGen) int8 [C][8][NP], zero padded
   int16_t* ep16;   // E' [C][8][N]   (KeyGen: E [C][N][8])
   int16_t* epp16;  // E'' [C][64]
-  uint16_t* bp16;  // B' = S'A + E' masked [C][8][N]   (KeyGen: B [C][N][8])
+  uint16_t* part;  // per-wave partial S'A (u16, mod 2^16) [C][NWV][8][N]; KeyGen: B [C][N][8]
   uint64_t* seeds; // per hs 16 u64: seedSE | k | pkh | mu'  (4 x 32 B)
   uint64_t* kk;    // per hs 4 u64: key fed to the final hash
-  uint8_t* tlo;    // A planes [SUB][N][NP] (lo limb), transposed: T[c][r] = limb(A[r][c])
-  uint8_t* thi;
 };
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -97,8 +98,8 @@ template <int N>
 size_t scratch_bytes_t(size_t C) {
   using P = FP<N>;
   const size_t W = (size_t)(P::SE_WORDS > P::KG_WORDS ? P::SE_WORDS : P::KG_WORDS);
-  return al256(C * W * 8) + al256(C * 8 * P::NP) + al256(C * 8 * N * 2) + al256(C * 64 * 2) + al256(C * 8 * N * 2) +
-         al256(C * 128) + al256(C * 32) + 2 * al256((size_t)SUB * N * P::NP);
+  return al256(C * W * 8) + al256(C * 8 * P::NP) + al256(C * 8 * N * 2) + al256(C * 64 * 2) +
+         al256(C * P::NWV * 8 * N * 2) + al256(C * 128) + al256(C * 32);
 }
 
 template <int N>
@@ -115,15 +116,11 @@ View<N> carve(void* base, size_t C) {
   p += al256(C * 8 * N * 2);
   v.epp16 = (int16_t*)p;
   p += al256(C * 64 * 2);
-  v.bp16 = (uint16_t*)p;
-  p += al256(C * 8 * N * 2);
+  v.part = (uint16_t*)p;
+  p += al256(C * P::NWV * 8 * N * 2);
   v.seeds = (uint64_t*)p;
   p += al256(C * 128);
   v.kk = (uint64_t*)p;
-  p += al256(C * 32);
-  v.tlo = p;
-  p += al256((size_t)SUB * N * P::NP);
-  v.thi = p;
   return v;
 }
 
@@ -259,28 +256,39 @@ __global__ __launch_bounds__(256) void k_fr_sample(const uint64_t* __restrict__ 
   }
 }
 
-// balanced limbs of a 16-bit value a: a == 256*hi + lo (mod 2^16), lo, hi in [-128, 127]
-__device__ __forceinline__ uint32_t limb_encode(uint32_t a) {
-  return ((a + 128u) & 0xFF00u) | (a & 0xFFu);  // byte0 = lo (two's complement), byte1 = hi
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// +128 on both 16-bit halves (v_pk_add_u16).  Balanced limbs of a 16-bit value a:
+// lo = a & 0xFF and hi = ((a + 128) >> 8) & 0xFF, read as int8, satisfy a == 256*hi + lo (mod 2^16).
+__device__ __forceinline__ uint32_t add80(uint32_t x) {
+  const u16x2 t = __builtin_bit_cast(u16x2, x) + (u16x2){0x80, 0x80};
+  return __builtin_bit_cast(uint32_t, t);
 }
 
-// Gen(A) (SHAKE variant): row r of handshake hs = SHAKE128(LE16(r) || seedA), 2N bytes.
-// Each 128-lane workgroup owns 128 consecutive rows of one handshake; per squeezed block
-// the rows' 84 limb-encoded values are staged in LDS [84][128] and written out as
-// transposed byte planes T_lo/T_hi[hs][c][r] with 16-byte stores (16 rows per store).
+// Gen(A) fused with S'A.  Row r of handshake hs = SHAKE128(LE16(r) || seedA) (2N bytes,
+// little-endian u16).  One wave owns 64 consecutive rows (lane = row) of one handshake;
+// per squeezed SHAKE128 block its 84 columns are limb-encoded into LDS as [c][r] and
+// contracted over the wave's rows on i8 MFMA:
+//   D(16x16) = X(16x64) . Y(64x16),  m = column c (16 per tile), n = k (8 used), K = row r,
+//   X[c][r] = limb(A[r][c]) from LDS, Y[r][k] = S'[k][r] (fixed per wave, kept in registers).
+// Lane l supplies m/n = l & 15 and the K slice 16*(l >> 4) .. +15 of both operands (the same
+// pairing of contraction indices in X and Y, so the result does not depend on the hardware's
+// order inside a fragment); D: col = l & 15 (k), row = 4*(l >> 4) + reg (c).
+// The wave's partial sum lo + 256*hi (mod 2^16) of 4 consecutive columns is one 8-byte store.
 template <int N>
-__global__ __launch_bounds__(128) void k_fr_gen_at(const uint8_t* __restrict__ seed_base, size_t seed_stride,
-                                                   size_t hs0, size_t nsub, uint8_t* __restrict__ tlo,
-                                                   uint8_t* __restrict__ thi) {
+__global__ __launch_bounds__(64) void k_fr_gen_mm(const uint8_t* __restrict__ seed_base, size_t seed_stride, size_t n,
+                                                  const int8_t* __restrict__ sp8, uint16_t* __restrict__ part) {
   using P = FP<N>;
-  constexpr int WGS_PER_HS = P::NP / 128;
-  __shared__ uint16_t st[84 * 128];
-  const size_t h = blockIdx.x / WGS_PER_HS;  // handshake within the sub-chunk
-  const int r0 = (int)(blockIdx.x % WGS_PER_HS) * 128;
-  if (h >= nsub) return;
-  const int r = r0 + threadIdx.x;
-  const bool live = r < N;
-  const uint8_t* sa = seed_base + (hs0 + h) * seed_stride;
+  __shared__ __attribute__((aligned(16))) uint16_t st[96 * ST_PITCH];
+  const size_t hs = blockIdx.x / P::NWV;
+  const int wv = (int)(blockIdx.x % P::NWV);
+  if (hs >= n) return;
+  const int lane = threadIdx.x;
+  const int r = wv * 64 + lane;
+  const int kq = lane & 15, ks = 16 * (lane >> 4);
+  v4i y = {0, 0, 0, 0};
+  if (kq < NBAR) y = *(const v4i*)(sp8 + (hs * NBAR + kq) * P::NP + wv * 64 + ks);  // zero past row N
+  const uint8_t* sa = seed_base + hs * seed_stride;
   uint64_t in[3];
   {
     const uint64_t s0 = ((const uint64_t*)sa)[0], s1 = ((const uint64_t*)sa)[1];
@@ -291,85 +299,59 @@ __global__ __launch_bounds__(128) void k_fr_gen_at(const uint8_t* __restrict__ s
   KState s;
   kzero(s);
   absorb_short<21, 3>(s, in, 18);
-  uint8_t* plo = tlo + h * (size_t)N * P::NP;
-  uint8_t* phi = thi + h * (size_t)N * P::NP;
+  uint16_t* prt = part + (hs * P::NWV + wv) * NBAR * N;
 #pragma unroll 1
   for (int b = 0; b < P::A_BLOCKS; ++b) {
     if (b) keccak_f(s);
     const int c0 = 84 * b;
-    const int nc = (N - c0) < 84 ? (N - c0) : 84;
+    const int nc = (N - c0) < 84 ? (N - c0) : 84;  // a multiple of 4 for every parameter set
 #pragma unroll
     for (int w = 0; w < 21; ++w) {
       const uint32_t lo = s.a[w].lo, hi = s.a[w].hi;
-      const uint32_t v[4] = {lo & 0xFFFF, lo >> 16, hi & 0xFFFF, hi >> 16};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (4 * w + e < nc) st[(4 * w + e) * 128 + threadIdx.x] = live ? (uint16_t)limb_encode(v[e]) : 0;
-    }
-    __syncthreads();
-    // nc columns x 8 groups of 16 rows
-    for (int task = threadIdx.x; task < nc * 8; task += 128) {
-      const int c = task >> 3, g = task & 7;
-      const uint4 a = *(const uint4*)&st[c * 128 + 16 * g];
-      const uint4 bb = *(const uint4*)&st[c * 128 + 16 * g + 8];
-      // even bytes -> lo plane, odd bytes -> hi plane
-      const uint32_t w8[8] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w};
-      uint32_t ol[4], oh[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ol[q] = __builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x06040200u);
-        oh[q] = __builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x07050301u);
+      // two values per dword: limb lo = low byte of the value, limb hi = high byte of
+      // (value + 128) (packed 16-bit add, no carry between the halves):
+      // al = [lo0 | hi0 << 8 | lo1 << 16 | hi1 << 24] for values 4w, 4w+1
+      const uint32_t al = __builtin_amdgcn_perm(add80(lo), lo, 0x07020500u);
+      const uint32_t ah = __builtin_amdgcn_perm(add80(hi), hi, 0x07020500u);
+      if (4 * w < nc) {
+        st[(4 * w + 0) * ST_PITCH + lane] = (uint16_t)al;
+        st[(4 * w + 1) * ST_PITCH + lane] = (uint16_t)(al >> 16);
+        st[(4 * w + 2) * ST_PITCH + lane] = (uint16_t)ah;
+        st[(4 * w + 3) * ST_PITCH + lane] = (uint16_t)(ah >> 16);
       }
-      const size_t off = (size_t)(c0 + c) * P::NP + r0 + 16 * g;
-      *(uint4*)(plo + off) = make_uint4(ol[0], ol[1], ol[2], ol[3]);
-      *(uint4*)(phi + off) = make_uint4(oh[0], oh[1], oh[2], oh[3]);
     }
-    __syncthreads();
-  }
-}
-
-// B'[k][c] = (sum_r S'[k][r] A[r][c] + E'[k][c]) mod q on i8 MFMA.
-// D(16x16) = X(16x64) . Y(64x16) with m = c (16 columns of A), n = k (8 used),
-// K = r:  X[c][r] = T[c][r] (limb planes), Y[r][k] = S'[k][r].  Lane l holds
-// m/n index l & 15 and K slice 16*(l >> 4) .. +15 of both operands (a consistent
-// pairing of the contraction index, so the result is independent of the
-// hardware's internal K order); D: col = l & 15, row = 4*(l >> 4) + reg.
-template <int N>
-__global__ __launch_bounds__(256) void k_fr_mm(size_t hs0, size_t nsub, const uint8_t* __restrict__ tlo,
-                                               const uint8_t* __restrict__ thi, const int8_t* __restrict__ sp8,
-                                               const int16_t* __restrict__ ep16, uint16_t* __restrict__ bp16) {
-  using P = FP<N>;
-  constexpr int TILES = N / 16;
-  constexpr int WG_PER_HS = (TILES + 3) / 4;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const size_t h = blockIdx.x / WG_PER_HS;
-  const int tile = (int)(blockIdx.x % WG_PER_HS) * 4 + wv;
-  if (h >= nsub || tile >= TILES) return;
-  const size_t hs = hs0 + h;
-  const int c0 = tile * 16;
-  const int m = lane & 15, ks = 16 * (lane >> 4);
-  const uint8_t* xl = tlo + h * (size_t)N * P::NP + (size_t)(c0 + m) * P::NP + ks;
-  const uint8_t* xh = thi + h * (size_t)N * P::NP + (size_t)(c0 + m) * P::NP + ks;
-  const bool kv = m < NBAR;
-  const int8_t* yp = sp8 + (hs * NBAR + (kv ? m : 0)) * P::NP + ks;
-  v4i acc_lo = {0, 0, 0, 0}, acc_hi = {0, 0, 0, 0};
-#pragma unroll 2
-  for (int r0 = 0; r0 < P::NP; r0 += 64) {
-    const v4i a_lo = *(const v4i*)(xl + r0);
-    const v4i a_hi = *(const v4i*)(xh + r0);
-    v4i y = *(const v4i*)(yp + r0);
-    if (!kv) y = v4i{0, 0, 0, 0};
-    acc_lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(a_lo, y, acc_lo, 0, 0, 0);
-    acc_hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(a_hi, y, acc_hi, 0, 0, 0);
-  }
-  if (kv) {
-    const int k = m;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int ntile = (nc + 15) >> 4;
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int c = c0 + 4 * (lane >> 4) + reg;
-      const uint32_t v = (uint32_t)(acc_lo[reg] + 256 * acc_hi[reg]) + (uint32_t)ep16[(hs * NBAR + k) * N + c];
-      bp16[(hs * NBAR + k) * N + c] = (uint16_t)(v & P::QMASK);
+    for (int t = 0; t < 6; ++t) {
+      if (t < ntile) {
+        const uint16_t* src = st + (16 * t + kq) * ST_PITCH + ks;
+        const uint4 a0 = *(const uint4*)src;        // rows ks .. ks+7
+        const uint4 a1 = *(const uint4*)(src + 8);  // rows ks+8 .. ks+15
+        const uint32_t w8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        v4i xl, xh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xl[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x06040200u);
+          xh[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x07050301u);
+        }
+        const v4i z = {0, 0, 0, 0};
+        const v4i dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, y, z, 0, 0, 0);
+        const v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, y, z, 0, 0, 0);
+        const int cl = 16 * t + 4 * (lane >> 4);
+        if (kq < NBAR && cl < nc) {
+          uint32_t v[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)dl[g] + ((uint32_t)dh[g] << 8)) & 0xFFFFu;
+          *(uint2*)(prt + kq * N + c0 + cl) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+        }
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -385,19 +367,23 @@ __device__ __forceinline__ uint32_t unpack_at(const uint8_t* p, size_t idx) {
   return (w >> sh) & ((1u << LOGQ) - 1);
 }
 
-// Pack cnt values (MSB-first, LOGQ bits each) starting at a byte-aligned bit offset.
-template <int LOGQ, typename Get>
-__device__ __forceinline__ void pack_run(uint8_t* dst, int cnt, Get get) {
-  uint64_t acc = 0;
-  int bits = 0, o = 0;
-  for (int i = 0; i < cnt; ++i) {
-    acc = (acc << LOGQ) | (get(i) & ((1u << LOGQ) - 1));
-    bits += LOGQ;
-    while (bits >= 8) {
-      dst[o++] = (uint8_t)(acc >> (bits - 8));
-      bits -= 8;
-    }
-  }
+// 8 LOGQ-bit values, MSB first, in LOGQ bytes (a group never straddles a byte boundary)
+template <int LOGQ>
+__device__ __forceinline__ void unpack8(const uint8_t* p, uint32_t v[8]) {
+  unsigned __int128 x = 0;
+#pragma unroll
+  for (int b = 0; b < LOGQ; ++b) x = (x << 8) | p[b];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (uint32_t)(x >> ((7 - i) * LOGQ)) & ((1u << LOGQ) - 1);
+}
+
+template <int LOGQ>
+__device__ __forceinline__ void pack8(const uint32_t v[8], uint8_t* p) {
+  unsigned __int128 x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x = (x << LOGQ) | (v[i] & ((1u << LOGQ) - 1));
+#pragma unroll
+  for (int b = 0; b < LOGQ; ++b) p[b] = (uint8_t)(x >> (8 * (LOGQ - 1 - b)));
 }
 
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
@@ -406,61 +392,115 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
   return x;
 }
 
-// V = S'B + E'', C = V + Encode(mu) (mod q); Pack(B') || Pack(C) -> out.
-// MODE 0 (encaps): out = ct, kk = k.  MODE 1 (decaps): ct' is packed into LDS,
-// compared with ct and select kk = (ct == ct') ? k' : s in constant time.
+// B' = (sum of the NWV partial S'A + E') mod q; V = S'B + E''; C = V + Encode(mu) (mod q);
+// ct = Pack(B') || Pack(C), staged in LDS.  One 256-thread workgroup per handshake.
+// MODE 0 (encaps): ct is stored with coalesced 8-byte stores, kk = k.
+// MODE 1 (decaps): ct' stays in LDS, is compared with the received ct, and
+// kk = (ct == ct') ? k' : s is selected in constant time.
 template <int N, int MODE>
-__global__ __launch_bounds__(64) void k_fr_pack(size_t n, const uint8_t* __restrict__ pk_base, size_t pk_stride,
-                                                const int8_t* __restrict__ sp8, const int16_t* __restrict__ epp16,
-                                                const uint16_t* __restrict__ bp16, const uint64_t* __restrict__ seeds,
-                                                const uint8_t* __restrict__ mu_base, size_t mu_stride,
-                                                uint8_t* __restrict__ out, const uint8_t* __restrict__ ct_in,
-                                                const uint8_t* __restrict__ s_base, size_t s_stride,
-                                                uint64_t* __restrict__ kk) {
+__global__ __launch_bounds__(256) void k_fr_pack(size_t n, const uint8_t* __restrict__ pk_base, size_t pk_stride,
+                                                 const int8_t* __restrict__ sp8, const int16_t* __restrict__ ep16,
+                                                 const int16_t* __restrict__ epp16, const uint16_t* __restrict__ part,
+                                                 const uint64_t* __restrict__ seeds, const uint8_t* __restrict__ mu_base,
+                                                 size_t mu_stride, uint8_t* __restrict__ ct_out,
+                                                 const uint8_t* __restrict__ ct_in, const uint8_t* __restrict__ s_base,
+                                                 size_t s_stride, uint64_t* __restrict__ kk) {
   using P = FP<N>;
+  constexpr int CTW = P::CT / 8;
+  __shared__ __attribute__((aligned(16))) uint16_t bsh[N * NBAR];  // B [j][i]
+  __shared__ __attribute__((aligned(16))) uint8_t cbuf[(P::CT + 15) / 16 * 16];
+  __shared__ uint32_t red[256];
+  __shared__ uint32_t cv[64];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
-  const int l = threadIdx.x;
-  const uint8_t* pkb = pk_base + hs * pk_stride + 16;  // packed B (N x 8)
-  // ---- V[k][i] for lane (k = l >> 3, i = l & 7)
-  const int k = l >> 3, i = l & 7;
-  const int8_t* sp = sp8 + (hs * NBAR + k) * P::NP;
-  uint32_t acc = (uint32_t)(int32_t)epp16[hs * 64 + l];
-  for (int j = 0; j < N; ++j) acc += (uint32_t)((int32_t)sp[j] * (int32_t)unpack_at<P::LOGQ>(pkb, (size_t)j * NBAR + i));
-  // Encode(mu): EB bits of mu at bit position EB*(8k + i)
-  __shared__ uint8_t cbuf[MODE ? P::CT : 1];  // decaps: re-encryption ciphertext stays on chip
-  const uint8_t* mu = mu_base + hs * mu_stride;
-  const int bit0 = P::EB * l;
-  uint32_t mv = 0;
+  const int t = threadIdx.x;
+  // 1. unpack B (N rows of 8 values = one LOGQ-byte group each)
+  const uint8_t* pkb = pk_base + hs * pk_stride + 16;
+  for (int g = t; g < N; g += 256) {
+    uint32_t v[8];
+    unpack8<P::LOGQ>(pkb + g * P::LOGQ, v);
+    *(uint4*)&bsh[g * 8] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
+  }
+  // 2. B' groups: partial sums (u16 pairs, lane-wise adds) + E', masked, packed into LDS
+  const uint16_t* pp = part + hs * P::NWV * NBAR * N;
+  const int16_t* ep = ep16 + hs * NBAR * N;
+  for (int g = t; g < N; g += 256) {
+    uint32_t lo[4], hi[4];
+    {
+      const uint4 e0 = *(const uint4*)(ep + 8 * g);
+      const uint32_t e[4] = {e0.x, e0.y, e0.z, e0.w};
 #pragma unroll
-  for (int b = 0; b < P::EB; ++b) mv |= (uint32_t)((mu[(bit0 + b) >> 3] >> ((bit0 + b) & 7)) & 1) << b;
-  const uint32_t cval = (acc + (mv << (P::LOGQ - P::EB))) & P::QMASK;
-  uint8_t* o = MODE ? cbuf : out + hs * P::CT;
-  // ---- Pack B' (8N values, [k][c] row-major): lane l packs values [l*N/8, (l+1)*N/8)
-  constexpr int PER = NBAR * N / 64;  // values per lane; PER*LOGQ is a multiple of 8
-  const uint16_t* bp = bp16 + hs * NBAR * N;
-  pack_run<P::LOGQ>(o + (size_t)l * PER * P::LOGQ / 8, PER, [&](int t) { return (uint32_t)bp[l * PER + t]; });
-  // ---- Pack C (64 values): lanes 0..7 pack 8 values each (8*LOGQ bits = LOGQ bytes)
-  __shared__ uint32_t cv[64];
-  cv[l] = cval;
+      for (int q = 0; q < 4; ++q) lo[q] = e[q] & 0xFFFF, hi[q] = e[q] >> 16;
+    }
+#pragma unroll 4
+    for (int w = 0; w < P::NWV; ++w) {
+      const uint4 x = *(const uint4*)(pp + (size_t)w * NBAR * N + 8 * g);
+      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lo[q] += xs[q] & 0xFFFF, hi[q] += xs[q] >> 16;
+    }
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[2 * q] = lo[q], v[2 * q + 1] = hi[q];
+    pack8<P::LOGQ>(v, cbuf + g * P::LOGQ);
+  }
   __syncthreads();
-  if (l < 8) pack_run<P::LOGQ>(o + P::LOGQ * N + l * P::LOGQ, 8, [&](int t) { return cv[8 * l + t]; });
+  // 3. V[k][i] = sum_j S'[k][j] B[j][i]: thread (k, i) x quarter of j
+  {
+    const int p = t & 63, k = p >> 3, i = p & 7, qj = t >> 6;
+    constexpr int JQ = N / 4;  // a multiple of 4
+    const int8_t* sp = sp8 + (hs * NBAR + k) * P::NP + qj * JQ;
+    const uint16_t* bc = bsh + qj * JQ * NBAR + i;
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (int j = 0; j < JQ; j += 4) {
+      const uint32_t s4 = *(const uint32_t*)(sp + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc += (uint32_t)((int32_t)(int8_t)(s4 >> (8 * e)) * (int32_t)bc[(j + e) * NBAR]);
+    }
+    red[t] = acc;
+  }
   __syncthreads();
+  if (t < 64) {
+    // Encode(mu): value t takes EB bits of mu at bit EB*t (little-endian bit order)
+    const uint8_t* mu = mu_base + hs * mu_stride;
+    const int bit0 = P::EB * t;
+    uint32_t mv = 0;
+#pragma unroll
+    for (int b = 0; b < P::EB; ++b) mv |= (uint32_t)((mu[(bit0 + b) >> 3] >> ((bit0 + b) & 7)) & 1) << b;
+    const uint32_t v = red[t] + red[t + 64] + red[t + 128] + red[t + 192] + (uint32_t)(int32_t)epp16[hs * 64 + t];
+    cv[t] = (v + (mv << (P::LOGQ - P::EB))) & P::QMASK;
+  }
+  __syncthreads();
+  if (t < 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = cv[8 * t + e];
+    pack8<P::LOGQ>(v, cbuf + P::LOGQ * N + t * P::LOGQ);
+  }
+  __syncthreads();
+  const uint64_t* cb = (const uint64_t*)cbuf;
   const uint64_t* sd = seeds + hs * 16;
   if (MODE == 0) {
-    if (l < P::SEC / 8) kk[hs * 4 + l] = sd[P::SEC / 8 + l];
+    uint64_t* o = (uint64_t*)(ct_out + hs * P::CT);
+    for (int x = t; x < CTW; x += 256) o[x] = cb[x];
+    if (t < P::SEC / 8) kk[hs * 4 + t] = sd[P::SEC / 8 + t];
     return;
   }
-  // ---- decaps: constant-time compare of ct' with ct, select k' or s
-  uint32_t diff = 0;
-  const uint8_t* c1 = ct_in + hs * P::CT;
-  for (int b = l; b < P::CT; b += 64) diff |= (uint32_t)(o[b] ^ c1[b]);
-  diff = wave_or(diff);
-  const uint64_t mask = (uint64_t)0 - (uint64_t)(diff == 0);  // computed without a branch on diff
-  if (l < P::SEC / 8) {
-    const uint64_t kp = sd[P::SEC / 8 + l];
-    const uint64_t sv = ((const uint64_t*)(s_base + hs * s_stride))[l];
-    kk[hs * 4 + l] = (kp & mask) | (sv & ~mask);
+  // 4. decaps: constant-time compare of ct' (LDS) with ct, select k' or s
+  const uint64_t* c1 = (const uint64_t*)(ct_in + hs * P::CT);
+  uint64_t d = 0;
+  for (int x = t; x < CTW; x += 256) d |= cb[x] ^ c1[x];
+  uint32_t diff = wave_or((uint32_t)d | (uint32_t)(d >> 32));
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = diff;
+  __syncthreads();
+  diff = red[0] | red[1] | red[2] | red[3];
+  const uint64_t mask = (uint64_t)0 - (uint64_t)(diff == 0);
+  if (t < P::SEC / 8) {
+    const uint64_t kp = sd[P::SEC / 8 + t];
+    const uint64_t sv = ((const uint64_t*)(s_base + hs * s_stride))[t];
+    kk[hs * 4 + t] = (kp & mask) | (sv & ~mask);
   }
 }
 
@@ -482,36 +522,65 @@ __global__ __launch_bounds__(256) void k_fr_ss(const uint8_t* __restrict__ ct, s
   for (int w = 0; w < P::SEC / 8; ++w) o[w] = kword(s, w);
 }
 
-// Decaps: M = C - B'S, mu' = Decode(M) -> seeds[12..]  (one wave per handshake)
+// Decaps: M = C - B'S, mu' = Decode(M) -> seeds[12..].  One 256-thread workgroup per
+// handshake: B' (from ct) and S^T (from sk) are staged in LDS with a padded pitch (rows land
+// on distinct banks), thread (i, k) x quarter of j accumulates, LDS reduction, wave 0 decodes.
 template <int N>
-__global__ __launch_bounds__(64) void k_fr_dec_m(size_t n, const uint8_t* __restrict__ ct,
-                                                 const uint8_t* __restrict__ sk, uint64_t* __restrict__ seeds) {
+__global__ __launch_bounds__(256) void k_fr_dec_m(size_t n, const uint8_t* __restrict__ ct,
+                                                  const uint8_t* __restrict__ sk, uint64_t* __restrict__ seeds) {
   using P = FP<N>;
+  constexpr int PIT = N + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t bq[NBAR * PIT];
+  __shared__ __attribute__((aligned(16))) uint16_t sq[NBAR * PIT];
+  __shared__ uint32_t red[256];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
-  const int l = threadIdx.x, i = l >> 3, k = l & 7;  // M[i][k]
+  const int t = threadIdx.x;
   const uint8_t* c = ct + hs * P::CT;
-  const uint8_t* st = sk + hs * P::SK + P::SEC + P::PK;  // S^T int16 LE [8][N]
-  uint32_t acc = 0;
-  for (int j = 0; j < N; ++j) {
-    const int32_t sv = (int16_t)((uint16_t)st[2 * (k * N + j)] | ((uint16_t)st[2 * (k * N + j) + 1] << 8));
-    acc += (uint32_t)((int32_t)unpack_at<P::LOGQ>(c, (size_t)i * N + j) * sv);
+  for (int g = t; g < N; g += 256) {  // B' group g = flat values 8g .. 8g+7 = row i, columns j .. j+7
+    uint32_t v[8];
+    unpack8<P::LOGQ>(c + g * P::LOGQ, v);
+    const int i = (8 * g) / N, j = (8 * g) % N;
+    *(uint4*)&bq[i * PIT + j] =
+        make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
   }
-  const uint32_t cv = unpack_at<P::LOGQ>(c + P::LOGQ * N, (size_t)l);
-  const uint32_t mval = (cv - acc) & P::QMASK;
-  const uint32_t t = ((mval + (1u << (P::LOGQ - P::EB - 1))) >> (P::LOGQ - P::EB)) & ((1u << P::EB) - 1);
-  // assemble EB*64 bits, lane l contributes bits [EB*l, EB*l + EB)
+  const uint64_t* sts = (const uint64_t*)(sk + hs * P::SK + P::SEC + P::PK);  // S^T int16 LE [8][N], 8-B aligned
+  for (int g = t; g < N; g += 256) {
+    const int k = (8 * g) / N, j = (8 * g) % N;
+    *(uint2*)&sq[k * PIT + j] = *(const uint2*)&sts[2 * g];
+    *(uint2*)&sq[k * PIT + j + 4] = *(const uint2*)&sts[2 * g + 1];
+  }
+  __syncthreads();
+  {
+    const int p = t & 63, i = p >> 3, k = p & 7, qj = t >> 6;
+    constexpr int JQ = N / 4;
+    const uint32_t* b2 = (const uint32_t*)&bq[i * PIT + qj * JQ];
+    const uint32_t* s2 = (const uint32_t*)&sq[k * PIT + qj * JQ];
+    uint32_t acc = 0;
+#pragma unroll 4
+    for (int j = 0; j < JQ / 2; ++j) {
+      const uint32_t bb = b2[j], ss = s2[j];
+      acc += (bb & 0xFFFF) * (uint32_t)(int32_t)(int16_t)(ss & 0xFFFF);
+      acc += (bb >> 16) * (uint32_t)(int32_t)(int16_t)(ss >> 16);
+    }
+    red[t] = acc;
+  }
+  __syncthreads();
+  if (t >= 64) return;
+  const uint32_t acc = red[t] + red[t + 64] + red[t + 128] + red[t + 192];
+  const uint32_t cval = unpack_at<P::LOGQ>(c + P::LOGQ * N, (size_t)t);
+  const uint32_t mval = (cval - acc) & P::QMASK;
+  const uint32_t dv = ((mval + (1u << (P::LOGQ - P::EB - 1))) >> (P::LOGQ - P::EB)) & ((1u << P::EB) - 1);
+  // assemble EB*64 bits: value t contributes bits [EB*t, EB*t + EB)
   uint64_t* mu = seeds + hs * 16 + 12;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
     uint64_t part = 0;
-    const int b = P::EB * l - 64 * w;
-    if (b >= 0 && b < 64) part = (uint64_t)t << b;
-    else if (b < 0 && b + P::EB > 0) part = (uint64_t)t >> (-b);
-    uint32_t lo = (uint32_t)part, hi = (uint32_t)(part >> 32);
-    lo = wave_or(lo);
-    hi = wave_or(hi);
-    if (l == 0 && w < (P::MU + 7) / 8) mu[w] = ((uint64_t)hi << 32) | lo;
+    const int b = P::EB * t - 64 * w;
+    if (b >= 0 && b < 64) part = (uint64_t)dv << b;
+    else if (b < 0 && b + P::EB > 0) part = (uint64_t)dv >> (-b);
+    const uint32_t lo = wave_or((uint32_t)part), hi = wave_or((uint32_t)(part >> 32));
+    if (t == 0 && w < (P::MU + 7) / 8) mu[w] = ((uint64_t)hi << 32) | lo;
   }
 }
 
@@ -595,30 +664,50 @@ __global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ 
   for (int k = 0; k < NBAR; ++k) bmat[(hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
 }
 
-// pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh   (one wave per handshake;
-// pkh is hashed by k_fr_kg_pkh afterwards)
+// pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh.  One 256-thread workgroup
+// per handshake; packed B is staged in LDS and copied out with 8-byte stores (pkh is hashed
+// by k_fr_kg_pkh afterwards; seedA and s were written by k_fr_kg_front).
 template <int N>
-__global__ __launch_bounds__(64) void k_fr_kg_pack(size_t n, const uint16_t* __restrict__ bmat,
-                                                   const int8_t* __restrict__ sp8, uint8_t* __restrict__ pk,
-                                                   uint8_t* __restrict__ sk) {
+__global__ __launch_bounds__(256) void k_fr_kg_pack(size_t n, const uint16_t* __restrict__ bmat,
+                                                    const int8_t* __restrict__ sp8, uint8_t* __restrict__ pk,
+                                                    uint8_t* __restrict__ sk) {
   using P = FP<N>;
+  __shared__ __attribute__((aligned(16))) uint8_t pbuf[(P::PK + 15) / 16 * 16];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
-  const int l = threadIdx.x;
-  constexpr int PER = NBAR * N / 64;
-  uint8_t* pkb = pk + hs * P::PK + 16;
+  const int t = threadIdx.x;
   const uint16_t* bm = bmat + hs * N * NBAR;
-  pack_run<P::LOGQ>(pkb + (size_t)l * PER * P::LOGQ / 8, PER, [&](int t) { return (uint32_t)bm[l * PER + t]; });
+  if (t < 2) ((uint64_t*)pbuf)[t] = ((const uint64_t*)(pk + hs * P::PK))[t];  // seedA
+  for (int g = t; g < N; g += 256) {
+    const uint4 x = *(const uint4*)(bm + 8 * g);
+    const uint32_t v[8] = {x.x & 0xFFFF, x.x >> 16, x.y & 0xFFFF, x.y >> 16,
+                           x.z & 0xFFFF, x.z >> 16, x.w & 0xFFFF, x.w >> 16};
+    pack8<P::LOGQ>(v, pbuf + 16 + g * P::LOGQ);
+  }
   __syncthreads();
-  // copy pk[16..] into sk, S^T as int16 LE
-  uint8_t* skp = sk + hs * P::SK + P::SEC;
-  for (int b = 16 + l; b < P::PK; b += 64) skp[b] = pk[hs * P::PK + b];
-  uint8_t* sts = sk + hs * P::SK + P::SEC + P::PK;
-  for (int t = l; t < NBAR * N; t += 64) {
-    const int k = t / N, j = t % N;
-    const int16_t v = sp8[(hs * NBAR + k) * P::NP + j];
-    sts[2 * t] = (uint8_t)v;
-    sts[2 * t + 1] = (uint8_t)((uint16_t)v >> 8);
+  uint64_t* po = (uint64_t*)(pk + hs * P::PK);
+  uint64_t* so = (uint64_t*)(sk + hs * P::SK + P::SEC);
+  const uint64_t* pb = (const uint64_t*)pbuf;
+  for (int x = t; x < P::PK / 8; x += 256) {
+    const uint64_t w = pb[x];
+    if (x >= 2) po[x] = w;
+    so[x] = w;
+  }
+  uint64_t* sto = (uint64_t*)(sk + hs * P::SK + P::SEC + P::PK);
+  for (int g = t; g < N; g += 256) {  // 8 S^T entries -> 16 bytes of int16 LE
+    const int k = (8 * g) / N, j = (8 * g) % N;
+    const uint2 raw = *(const uint2*)(sp8 + (hs * NBAR + k) * P::NP + j);
+    const uint32_t b8[2] = {raw.x, raw.y};
+    uint64_t o[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint64_t acc = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc |= (uint64_t)(uint16_t)(int16_t)(int8_t)(b8[h] >> (8 * e)) << (16 * e);
+      o[h] = acc;
+    }
+    sto[2 * g] = o[0];
+    sto[2 * g + 1] = o[1];
   }
 }
 
@@ -640,17 +729,12 @@ __global__ __launch_bounds__(256) void k_fr_kg_pkh(const uint8_t* __restrict__ p
 inline unsigned blocks_for(size_t t, int per = 256) { return (unsigned)((t + per - 1) / per); }
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
-// S'A + E' for every handshake of the chunk, SUB handshakes at a time
+// per-wave partial sums of S'A for every handshake of the chunk (Gen(A) fused)
 template <int N>
 void launch_sa(const View<N>& v, const uint8_t* seed_base, size_t seed_stride, size_t n, hipStream_t st) {
   using P = FP<N>;
-  for (size_t h0 = 0; h0 < n; h0 += SUB) {
-    const size_t m = n - h0 < (size_t)SUB ? n - h0 : (size_t)SUB;
-    QRK_LAUNCH("k_fr_gen_at", st, k_fr_gen_at<N>, dim3((unsigned)(m * (P::NP / 128))), dim3(128), 0, st, seed_base,
-               seed_stride, h0, m, v.tlo, v.thi);
-    QRK_LAUNCH("k_fr_mm", st, k_fr_mm<N>, dim3((unsigned)(m * ((N / 16 + 3) / 4))), dim3(256), 0, st, h0, m, v.tlo,
-               v.thi, v.sp8, v.ep16, v.bp16);
-  }
+  QRK_LAUNCH("k_fr_gen_mm", st, k_fr_gen_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, seed_base, seed_stride,
+             n, v.sp8, v.part);
 }
 
 template <int N>
@@ -665,8 +749,8 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N>(v, pk, P::PK, n, st);
-  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(64), 0, st, n, pk, (size_t)P::PK, v.sp8,
-             v.epp16, v.bp16, v.seeds, mu, (size_t)P::MU, ct, nullptr, nullptr, (size_t)0, v.kk);
+  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
+             v.ep16, v.epp16, v.part, v.seeds, mu, (size_t)P::MU, ct, nullptr, nullptr, (size_t)0, v.kk);
   QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
   return hipGetLastError();
 }
@@ -677,15 +761,15 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   const size_t C = round64(n);
   View<N> v = carve<N>(scratch, C);
   const uint8_t* pk_in_sk = sk + P::SEC;
-  QRK_LAUNCH("k_fr_dec_m", st, k_fr_dec_m<N>, dim3((unsigned)n), dim3(64), 0, st, n, ct, sk, v.seeds);
+  QRK_LAUNCH("k_fr_dec_m", st, k_fr_dec_m<N>, dim3((unsigned)n), dim3(256), 0, st, n, ct, sk, v.seeds);
   QRK_LAUNCH("k_fr_g2_dec", st, k_fr_g2_dec<N>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.seeds);
   QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream<N>, dim3(blocks_for(n)), dim3(256), 0, st, v.seeds, n, 0x96,
              P::SE_WORDS, P::SE_WORDS, v.raw);
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N>(v, pk_in_sk, P::SK, n, st);
-  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(64), 0, st, n, pk_in_sk, (size_t)P::SK,
-             v.sp8, v.epp16, v.bp16, v.seeds, (const uint8_t*)(v.seeds + 12), (size_t)128, nullptr, ct, sk,
+  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
+             v.sp8, v.ep16, v.epp16, v.part, v.seeds, (const uint8_t*)(v.seeds + 12), (size_t)128, nullptr, ct, sk,
              (size_t)P::SK, v.kk);
   QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
   return hipGetLastError();
@@ -704,8 +788,8 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
   QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
-             v.sp8, v.ep16, v.bp16);
-  QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(64), 0, st, n, v.bp16, v.sp8, pk, sk);
+             v.sp8, v.ep16, v.part);
+  QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(256), 0, st, n, v.part, v.sp8, pk, sk);
   QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, n, sk);
   return hipGetLastError();
 }

@@ -161,6 +161,11 @@ class BatchKEM:
                     "decaps")
         return ss
 
+    @property
+    def effective_chunk(self) -> int:
+        """Handshakes per internal chunk for this algorithm (FrodoKEM caps it by scratch size)."""
+        return int(LIB.qrk_ctx_effective_chunk(self._ctx, self.alg.encode()))
+
     def set_streams(self, streams: int) -> None:
         """2: fork independent kernel chains onto a side stream (default); 1: serial."""
         self._check(LIB.qrk_ctx_set_streams(self._ctx, streams), "set_streams")
