@@ -31,7 +31,6 @@ constexpr int QINV = 62209;  // q^-1 mod 2^16
 constexpr int XOF_W = 64;    // 256 int16 sampled coefficients (512 B) per matrix entry
 constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
 constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
-constexpr int R2 = 1353;       // R^2 mod q            (to Montgomery form)
 
 // ---------------------------------------------------------------- tables
 constexpr int powq(int b, int e) {
@@ -64,6 +63,23 @@ constexpr Tables make_tables() {
 constexpr Tables TABC = make_tables();          // compile-time indexed twiddles
 __constant__ Tables TABD = make_tables();       // lane-indexed twiddles
 
+// Plain-domain twiddles as fp32 (centered integers, exact): the NTTs run in fp32.
+struct TablesF {
+  float z[128];  // zeta^br7(i) mod q
+  float g[128];  // gamma_i = zeta^(2 br7(i) + 1) mod q
+};
+constexpr TablesF make_tables_f() {
+  TablesF t{};
+  for (int i = 0; i < 128; ++i) {
+    t.z[i] = (float)centered(powq(17, br7(i)));
+    t.g[i] = (float)centered(powq(17, 2 * br7(i) + 1));
+  }
+  return t;
+}
+constexpr TablesF TABFC = make_tables_f();
+__constant__ TablesF TABFD = make_tables_f();
+constexpr float INV128F = (float)centered(3303);  // 128^-1 mod q (plain domain)
+
 // ---------------------------------------------------------------- arithmetic
 // Signed Montgomery reduction, R = 2^16: returns a * R^-1 mod q, |r| < 2^15 + q/2.
 // 4 full-rate VALU ops: v_mul_u32_u24, v_bfe_i32, v_mad_i32_i24, v_ashrrev.
@@ -81,6 +97,46 @@ __device__ __forceinline__ int canon(int a) {
   const int r = barrett(a);
   return r + ((r >> 31) & Q);
 }
+// ---- fp32 modular arithmetic (every value is an exact integer below 2^24)
+// MAGIC = 1.5 * 2^23: x + MAGIC rounds x to an integer (round-to-nearest-even), and
+// for |x| < 2^22 the bit pattern of x + MAGIC is 0x4B400000 + x, so its low 16 bits
+// are x as int16.  All ops below are full-rate on gfx950 (v_mul/v_add/v_fmaak/v_fmamk
+// _f32), unlike the 24/32-bit integer multiplies (half rate).
+constexpr float QF = 3329.0f;
+constexpr float QINVF = 1.0f / 3329.0f;
+constexpr float MAGIC = 12582912.0f;
+// x mod q, centered: |result| <= 1665 for |x| < 2^24 (|x / q - rint| <= 1/2 + 3e-4)
+__device__ __forceinline__ float reduce_f(float x) {
+  const float t = __builtin_fmaf(x, QINVF, MAGIC) - MAGIC;
+  return __builtin_fmaf(t, -QF, x);
+}
+// x * z mod q, centered, exact when |x * z| < 2^24 (for |z| <= 1664: |x| < 10082):
+// the product is exact, the fma computes p - t q with a single rounding of an integer < 2^24.
+__device__ __forceinline__ float modmul_f(float x, float z) {
+  const float p = x * z;
+  const float t = __builtin_fmaf(p, QINVF, MAGIC) - MAGIC;
+  return __builtin_fmaf(t, -QF, p);
+}
+__device__ __forceinline__ float i2f(int x) {  // |x| < 2^22
+  return __int_as_float(0x4B400000 + x) - MAGIC;
+}
+__device__ __forceinline__ int f2i(float x) {  // exact integer, |x| < 2^22
+  return __float_as_int(x + MAGIC) - 0x4B400000;
+}
+__device__ __forceinline__ uint32_t f2bits(float x) {  // low 16 bits = x as int16
+  return __float_as_uint(x + MAGIC);
+}
+// canonical [0, q) integer of an exact fp32 integer
+__device__ __forceinline__ int canon_f(float x) {
+  const int r = f2i(reduce_f(x));
+  return r + ((r >> 31) & Q);
+}
+// basemul accumulator (|acc| < 2^31) -> centered residue: acc = hi 2^16 + lo with
+// 2^16 = -1044 (mod q), |hi * 1044 + lo| < 5.1e6 (exact), then one reduction
+__device__ __forceinline__ float acc_to_f(int acc) {
+  return reduce_f(__builtin_fmaf(i2f(acc >> 16), -1044.0f, i2f(acc & 0xFFFF)));
+}
+
 // Compress_d(x) = round(2^d x / q) mod 2^d for x in [0, q): exact via 24-bit mulhi
 template <int D>
 __device__ __forceinline__ int compress(int x) {
@@ -123,16 +179,17 @@ __device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, i
 // with probability ~0.993, rarely 4).  Compaction happens in the producer:
 // every candidate is written to a 16-entry per-lane LDS ring at the running
 // count (a rejected one is simply overwritten by the next), and each completed
-// 8-coefficient chunk is flushed as one 16-byte store.  Output: 256 int16
-// coefficients per entry in a 64-entry tiled layout (chunk c of entry i at
-// ((i/64)*32 + c)*64 + i%64, 16-byte units), so the consumer reads them
-// without any parsing.  inst = (x*K + y) * C + hs.
-constexpr int RING_DW = 10;  // per-lane ring stride in dwords (40 B: 8-B aligned, 2-way banked)
+// 8-coefficient chunk is flushed as one 16-byte store.  The ring is
+// lane-interleaved (entry i of lane l at dword i*64 + l of the wave's ring), so
+// every lane always hits its own LDS bank: the random per-lane write offsets
+// never conflict.  Output: 256 int16 coefficients per entry in a 64-entry tiled
+// layout (chunk c of entry i at ((i/64)*32 + c)*64 + i%64, 16-byte units), so
+// the consumer reads them without any parsing.  inst = (x*K + y) * C + hs.
 constexpr int MAX_XOF_BLOCKS = 16;
 
 // Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
 // flushing completed 8-coefficient chunks to dst.
-__device__ __forceinline__ void compact_block(const KState& s, uint16_t* ring, int& cnt, uint4* dst) {
+__device__ __forceinline__ void compact_block(const KState& s, uint32_t* ring, int& cnt, uint4* dst) {
 #pragma unroll
   for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
     uint32_t d[3];
@@ -144,16 +201,22 @@ __device__ __forceinline__ void compact_block(const KState& s, uint16_t* ring, i
     int c[8];
     split12(d[0], d[1], d[2], c);
     const int before = cnt;
+    // cnt kept pre-scaled by 256 (the byte stride of one ring entry): per candidate
+    // one and + add for the address and cmp + cndmask + add for the count
+    int pos = cnt << 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      ring[cnt & 15] = (uint16_t)c[e];
-      cnt += c[e] < Q;
+      *(uint32_t*)((char*)ring + (pos & 0xF00)) = (uint32_t)c[e];
+      pos += c[e] < Q ? 256 : 0;
     }
+    cnt = pos >> 8;
     const int ch = before >> 3;
     if ((cnt >> 3) != ch && ch < 32) {
-      const uint2 lo = *(const uint2*)(ring + (ch & 1) * 8);
-      const uint2 hi = *(const uint2*)(ring + (ch & 1) * 8 + 4);
-      dst[ch * 64] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      const uint32_t* r = ring + (ch & 1) * 8 * 64;
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = r[(2 * j) * 64] | (r[(2 * j + 1) * 64] << 16);
+      dst[ch * 64] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
@@ -167,8 +230,8 @@ template <int K, bool FIX>
 __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
                                              size_t n, size_t C, uint4* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
-  __shared__ uint32_t ring_all[256 * RING_DW];
-  uint16_t* ring = (uint16_t*)(ring_all + threadIdx.x * RING_DW);
+  __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
+  uint32_t* ring = ring_all + (threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63);
   const size_t stride = FIX ? (size_t)gridDim.x * 256 : 0;
   size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t limit = FIX ? (size_t)*nfix : (size_t)K * K * C;
@@ -476,6 +539,143 @@ __device__ __forceinline__ void ntt_inv(P16& p, int* buf, int L) {
   for (int m = 0; m < 16; ++m) p.v[m] = fqmul(p.v[m], F_SCALE);
 }
 
+// ---- fp32 NTTs (plain domain).  Same data movement as the integer versions above.
+struct PF16 {
+  float v[16];
+};
+
+__device__ __forceinline__ void stride_to_contig_f(PF16& p, float* buf, int L) {
+#pragma unroll
+  for (int m = 0; m < 16; ++m) buf[L + 17 * m] = p.v[m];
+  gsync();
+#pragma unroll
+  for (int t = 0; t < 16; ++t) p.v[t] = buf[17 * L + t];
+  gsync();
+}
+__device__ __forceinline__ void contig_to_stride_f(PF16& p, float* buf, int L) {
+#pragma unroll
+  for (int t = 0; t < 16; ++t) buf[17 * L + t] = p.v[t];
+  gsync();
+#pragma unroll
+  for (int m = 0; m < 16; ++m) p.v[m] = buf[L + 17 * m];
+  gsync();
+}
+
+// FIPS 203 Alg. 9 in fp32.  In: stride layout (v[m] = f[L+16m]), |f| <= B0.
+// Out: contiguous layout (v[t] = f[16L+t]).  Each layer adds at most 1665 to the
+// bound and a layer's twiddle products must stay below 2^24 (|input| < 10082):
+// B0 <= 3 (CBD) -> 3 + 6 * 1665 = 9993 before the last layer, output <= 11658.
+// MIDRED (inputs up to q, e.g. decompressed u): reduce everything after layer 4;
+// output <= 4 * 1665.
+template <bool MIDRED>
+__device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
+#pragma unroll
+  for (int lg = 0; lg < 4; ++lg) {
+    const int step = 8 >> lg;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (((m / step) & 1) == 0) {
+        const float t = modmul_f(p.v[m + step], TABFC.z[(1 << lg) + m / (2 * step)]);
+        p.v[m + step] = p.v[m] - t;
+        p.v[m] = p.v[m] + t;
+      }
+    }
+  }
+  if (MIDRED) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) p.v[m] = reduce_f(p.v[m]);
+  }
+  stride_to_contig_f(p, buf, L);
+  {
+    const float z = TABFD.z[16 + L];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float u = modmul_f(p.v[t + 8], z);
+      p.v[t + 8] = p.v[t] - u;
+      p.v[t] = p.v[t] + u;
+    }
+  }
+  {
+    const float z0 = TABFD.z[32 + 2 * L], z1 = TABFD.z[33 + 2 * L];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 2) & 1) == 0) {
+        const float u = modmul_f(p.v[t + 4], t < 8 ? z0 : z1);
+        p.v[t + 4] = p.v[t] - u;
+        p.v[t] = p.v[t] + u;
+      }
+    }
+  }
+  {
+    float z[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z[s] = TABFD.z[64 + 4 * L + s];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 1) & 1) == 0) {
+        const float u = modmul_f(p.v[t + 2], z[t >> 2]);
+        p.v[t + 2] = p.v[t] - u;
+        p.v[t] = p.v[t] + u;
+      }
+    }
+  }
+}
+
+// FIPS 203 Alg. 10 in fp32 (including the 128^-1 scaling).  In: contiguous, |f| <= 1665.
+// Out: stride layout, |f| <= 1665.  Gentleman-Sande sums double per layer; the sums of
+// every second layer are reduced, so |y - x| <= 6660 at every twiddle product.
+__device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
+  {
+    float z[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) z[s] = TABFD.z[127 - 4 * L - s];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 1) & 1) == 0) {
+        const float x = p.v[t], y = p.v[t + 2];
+        p.v[t] = x + y;
+        p.v[t + 2] = modmul_f(y - x, z[t >> 2]);
+      }
+    }
+  }
+  {
+    const float z0 = TABFD.z[63 - 2 * L], z1 = TABFD.z[62 - 2 * L];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      if (((t >> 2) & 1) == 0) {
+        const float x = p.v[t], y = p.v[t + 4];
+        p.v[t] = reduce_f(x + y);
+        p.v[t + 4] = modmul_f(y - x, t < 8 ? z0 : z1);
+      }
+    }
+  }
+  {
+    const float z = TABFD.z[31 - L];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float x = p.v[t], y = p.v[t + 8];
+      p.v[t] = x + y;
+      p.v[t + 8] = modmul_f(y - x, z);
+    }
+  }
+  contig_to_stride_f(p, buf, L);
+#pragma unroll
+  for (int lg = 3; lg >= 0; --lg) {
+    const int step = 8 >> lg;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (((m / step) & 1) == 0) {
+        const float zeta = TABFC.z[(2 << lg) - 1 - m / (2 * step)];
+        const float x = p.v[m], y = p.v[m + step];
+        p.v[m] = ((lg & 1) == 1) ? reduce_f(x + y) : x + y;  // layers 4 and 6 reduce their sums
+        p.v[m + step] = modmul_f(y - x, zeta);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) p.v[m] = modmul_f(p.v[m], INV128F);
+}
+
 // ---- base-case multiplication (FIPS 203 Alg. 11/12) on packed int16 pairs
 // A coefficient pair (a0, a1) lives in one dword (lo, hi) -- exactly the
 // producer's sampled layout.  For the other operand b we precompute
@@ -506,6 +706,20 @@ __device__ __forceinline__ BOp make_bop(const P16& b, int L) {
   return r;
 }
 
+// From an fp32 NTT output (|b| <= 11658, fits int16): B0 = (b0, b1 gamma mod q),
+// B1 = (b1, b0).  b1 is reduced before the gamma product to keep it below 2^24.
+__device__ __forceinline__ BOp make_bop_f(const PF16& b, int L) {
+  BOp r;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t e0 = f2bits(b.v[2 * u]), e1 = f2bits(b.v[2 * u + 1]);
+    const uint32_t g = f2bits(modmul_f(reduce_f(b.v[2 * u + 1]), TABFD.g[8 * L + u]));
+    r.b0[u] = pack16((int)e0, (int)g);
+    r.b1[u] = pack16((int)e1, (int)e0);
+  }
+  return r;
+}
+
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s, a), __builtin_bit_cast(v2s, b), c, false);
 }
@@ -519,31 +733,50 @@ __device__ __forceinline__ void basemul_acc(int acc[16], const PK8& a, const BOp
   }
 }
 
-// CBD_eta from the PRF instance's raw words; contiguous layout.
+// Split CBD: the PRF words are loaded first (so a caller can prefetch them one
+// stage ahead) and expanded straight to fp32.
+struct CbdRaw {
+  uint32_t d[3];
+};
 template <int ETA>
-__device__ __forceinline__ void cbd(P16& p, const uint64_t* __restrict__ prf, size_t inst, int L) {
+__device__ __forceinline__ CbdRaw cbd_load(const uint64_t* __restrict__ prf, size_t inst, int L) {
+  CbdRaw r;
   if constexpr (ETA == 2) {
     const uint64_t w = prf[tidx(inst, L, PRF_W)];
-    const uint32_t d[2] = {(uint32_t)w, (uint32_t)(w >> 32)};
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const uint32_t f = (d[t >> 3] >> (4 * (t & 7))) & 0xF;
-      p.v[t] = (int)__popc(f & 3u) - (int)__popc(f & 0xCu);
-    }
+    r.d[0] = (uint32_t)w, r.d[1] = (uint32_t)(w >> 32), r.d[2] = 0;
   } else {
     const int wi = (3 * L) >> 1;
     const uint64_t a = prf[tidx(inst, wi, PRF_W)], b = prf[tidx(inst, wi + 1, PRF_W)];
     const bool odd = L & 1;
-    const uint32_t d0 = odd ? (uint32_t)(a >> 32) : (uint32_t)a;
-    const uint32_t d1 = odd ? (uint32_t)b : (uint32_t)(a >> 32);
-    const uint32_t d[3] = {d0, d1, odd ? (uint32_t)(b >> 32) : (uint32_t)b};
+    r.d[0] = odd ? (uint32_t)(a >> 32) : (uint32_t)a;
+    r.d[1] = odd ? (uint32_t)b : (uint32_t)(a >> 32);
+    r.d[2] = odd ? (uint32_t)(b >> 32) : (uint32_t)b;
+  }
+  return r;
+}
+// eta = 2 in SWAR form: per nibble (a0 a1 b0 b1), x holds a0+a1 and b0+b1 in two bit
+// pairs, y = (a0+a1) + 4 - (b0+b1) per nibble (no borrow), coefficient = nibble - 4,
+// built as an fp32 directly (0x4B400000 | nibble is 2^23 * 1.5 + nibble).
+template <int ETA>
+__device__ __forceinline__ void cbd_f(PF16& p, const CbdRaw& r) {
+  if constexpr (ETA == 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t d = r.d[h];
+      const uint32_t x = (d & 0x55555555u) + ((d >> 1) & 0x55555555u);
+      const uint32_t y = (x & 0x33333333u) + 0x44444444u - ((x >> 2) & 0x33333333u);
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+        p.v[8 * h + t] = __uint_as_float(((y >> (4 * t)) & 0xFu) | 0x4B400000u) - (MAGIC + 4.0f);
+    }
+  } else {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const int bit = 6 * t, i = bit >> 5, sh = bit & 31;
-      uint32_t f = d[i] >> sh;
-      if (sh + 6 > 32) f |= d[i + 1] << (32 - sh);
+      uint32_t f = r.d[i] >> sh;
+      if (sh + 6 > 32) f |= r.d[i + 1] << (32 - sh);
       f &= 0x3F;
-      p.v[t] = (int)__popc(f & 7u) - (int)__popc(f & 0x38u);
+      p.v[t] = i2f((int)__popc(f & 7u) - (int)__popc(f & 0x38u));
     }
   }
 }
@@ -723,13 +956,14 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
   BOp sb[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
+    PF16 f;
+    cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L));
+    contig_to_stride_f(f, (float*)g.poly, L);
+    ntt_fwd_f<false>(f, (float*)g.poly, L);
+    sb[j] = make_bop_f(f, L);
     P16 t;
-    cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
-    contig_to_stride(t, g.poly, L);
-    ntt_fwd(t, g.poly, L);
-    sb[j] = make_bop(t, L);
 #pragma unroll
-    for (int x = 0; x < 16; ++x) t.v[x] = canon(t.v[x]);
+    for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
     if (active) encode12(t, dk + 384 * j, L);
   }
 #pragma unroll 1
@@ -741,13 +975,13 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
     for (int j = 0; j < K; ++j) {
       basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(j * K + i) * C + hs, L), sb[j]);
     }
-    P16 e;
-    cbd<P<K>::ETA1>(e, prf, (size_t)(K + i) * C + hs, L);
-    contig_to_stride(e, g.poly, L);
-    ntt_fwd(e, g.poly, L);
+    PF16 ef;
+    cbd_f<P<K>::ETA1>(ef, cbd_load<P<K>::ETA1>(prf, (size_t)(K + i) * C + hs, L));
+    contig_to_stride_f(ef, (float*)g.poly, L);
+    ntt_fwd_f<false>(ef, (float*)g.poly, L);
     P16 t;
 #pragma unroll
-    for (int x = 0; x < 16; ++x) t.v[x] = canon(fqmul(mont_reduce(acc[x]), R2) + e.v[x]);
+    for (int x = 0; x < 16; ++x) t.v[x] = canon_f(acc_to_f(acc[x]) + ef.v[x]);
     if (active) {
       encode12(t, ek + 384 * i, L);
       encode12(t, dk + 384 * K + 384 * i, L);
@@ -778,33 +1012,48 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
   uint32_t diff = 0;
 
   BOp yb[K];
+  {
+    CbdRaw yr[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    P16 t;
-    cbd<P<K>::ETA1>(t, prf, (size_t)j * C + hs, L);
-    contig_to_stride(t, g.poly, L);
-    ntt_fwd(t, g.poly, L);
-    yb[j] = make_bop(t, L);
+    for (int j = 0; j < K; ++j) yr[j] = cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      PF16 f;
+      cbd_f<P<K>::ETA1>(f, yr[j]);
+      contig_to_stride_f(f, (float*)g.poly, L);
+      ntt_fwd_f<false>(f, (float*)g.poly, L);
+      yb[j] = make_bop_f(f, L);
+    }
   }
-  // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j)
+  // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
+  // Row i+1's matrix entries and the next CBD words are loaded one row ahead.
+  PK8 an[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)j * C + hs, L);
+  CbdRaw er = cbd_load<P<K>::ETA2>(prf, (size_t)K * C + hs, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(i * K + j) * C + hs, L), yb[j]);
+    for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
+    const CbdRaw ecur = er;
+    if (i + 1 < K) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hs, L);
     }
+    er = cbd_load<P<K>::ETA2>(prf, (size_t)(K + i + 1) * C + hs, L);  // e1_{i+1}, or e2 after the last row
+    PF16 uf;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) uf.v[t] = acc_to_f(acc[t]);
+    ntt_inv_f(uf, (float*)g.poly, L);
+    stride_to_contig_f(uf, (float*)g.poly, L);
+    PF16 ef;
+    cbd_f<P<K>::ETA2>(ef, ecur);
     P16 u;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) u.v[t] = mont_reduce(acc[t]);
-    ntt_inv(u, g.poly, L);
-    stride_to_contig(u, g.poly, L);
-    P16 e;
-    cbd<P<K>::ETA2>(e, prf, (size_t)(K + i) * C + hs, L);
-#pragma unroll
-    for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon(u.v[t] + e.v[t]));
+    for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon_f(uf.v[t] + ef.v[t]));
     pack_bits<DU>(u, g, L);
     flush_bits<DU>(g, c + 32 * DU * i, MODE ? c + 32 * DU * i : nullptr, diff, active, L);
   }
@@ -818,19 +1067,20 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
     for (int j = 0; j < K; ++j) {
       basemul_acc(acc, decode12(ek + 384 * j, bad, L), yb[j]);
     }
-    P16 v;
+    PF16 vf;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) v.v[t] = mont_reduce(acc[t]);
-    ntt_inv(v, g.poly, L);
-    stride_to_contig(v, g.poly, L);
-    P16 e;
-    cbd<P<K>::ETA2>(e, prf, (size_t)(2 * K) * C + hs, L);
+    for (int t = 0; t < 16; ++t) vf.v[t] = acc_to_f(acc[t]);
+    ntt_inv_f(vf, (float*)g.poly, L);
+    stride_to_contig_f(vf, (float*)g.poly, L);
+    PF16 ef;
+    cbd_f<P<K>::ETA2>(ef, er);  // e2
     const uint8_t* m = m_base + hs * m_stride;
     const uint32_t mb = (uint32_t)m[2 * L] | ((uint32_t)m[2 * L + 1] << 8);
+    P16 v;
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      const int mu = ((mb >> t) & 1) ? (Q + 1) / 2 : 0;
-      v.v[t] = compress<DV>(canon(v.v[t] + e.v[t] + mu));
+      const float mu = ((mb >> t) & 1) ? (float)((Q + 1) / 2) : 0.0f;
+      v.v[t] = compress<DV>(canon_f(vf.v[t] + ef.v[t] + mu));
     }
     pack_bits<DV>(v, g, L);
     flush_bits<DV>(g, c + 32 * DU * K, MODE ? c + 32 * DU * K : nullptr, diff, active, L);
@@ -872,23 +1122,24 @@ __global__ __launch_bounds__(256) void k_decrypt_core(size_t n, const uint8_t* _
   for (int j = 0; j < K; ++j) {
     P16 u;
     load_bits<DU>(u, c + 32 * DU * j, g, L);
+    PF16 uf;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) u.v[t] = decompress<DU>(u.v[t]);
-    contig_to_stride(u, g.poly, L);
-    ntt_fwd(u, g.poly, L);
-    basemul_acc(acc, decode12(dk + 384 * j, bad, L), make_bop(u, L));
+    for (int t = 0; t < 16; ++t) uf.v[t] = i2f(decompress<DU>(u.v[t]));
+    contig_to_stride_f(uf, (float*)g.poly, L);
+    ntt_fwd_f<true>(uf, (float*)g.poly, L);
+    basemul_acc(acc, decode12(dk + 384 * j, bad, L), make_bop_f(uf, L));
   }
-  P16 w;
+  PF16 w;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) w.v[t] = mont_reduce(acc[t]);
-  ntt_inv(w, g.poly, L);
-  stride_to_contig(w, g.poly, L);
+  for (int t = 0; t < 16; ++t) w.v[t] = acc_to_f(acc[t]);
+  ntt_inv_f(w, (float*)g.poly, L);
+  stride_to_contig_f(w, (float*)g.poly, L);
   P16 v;
   load_bits<DV>(v, c + 32 * DU * K, g, L);
   uint32_t bits = 0;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
-    const int x = canon(decompress<DV>(v.v[t]) - w.v[t]);
+    const int x = canon_f(i2f(decompress<DV>(v.v[t])) - w.v[t]);
     bits |= (uint32_t)compress<1>(x) << t;
   }
   if (active) ((uint16_t*)(mprime + hs * 4))[L] = (uint16_t)bits;

@@ -106,6 +106,36 @@ MKK(lshl_add, "v_lshl_add_u32 %0, %0, 3, %1", seed)
 MKK(ashr, "v_ashrrev_i32 %0, 16, %0 ; %1", seed)
 MKK(pk_add_u16, "v_pk_add_u16 %0, %0, %1", seed)
 MKK(pk_mul_lo_u16, "v_pk_mul_lo_u16 %0, %0, %1", seed)
+MKK(fmac_f32, "v_fmac_f32 %0, %1, %1", 0x3f000000u)
+MKK(fmaak_f32, "v_fmaak_f32 %0, %0, %1, 0x3f000000", 0x3f000000u)
+MKK(add_f32, "v_add_f32 %0, %0, %1", 0x3f000000u)
+MKK(cvt_f32_i32, "v_cvt_f32_i32 %0, %0 ; %1", 0u)
+MKK(cvt_i32_f32, "v_cvt_i32_f32 %0, %0 ; %1", 0u)
+MKK(mad_i32_i16, "v_mad_i32_i16 %0, %0, %1, %1", seed)
+MKK(mad_u32_u16, "v_mad_u32_u16 %0, %0, %1, %1", seed)
+MKK(mul_hi_i32, "v_mul_hi_i32 %0, %0, %1", seed)
+MKK(pk_mad_i16, "v_pk_mad_i16 %0, %0, %1, %1", seed)
+MKK(sub_sdwa, "v_sub_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0", seed)
+MKK(bfe_i32, "v_bfe_i32 %0, %0, 0, 16 ; %1", seed)
+MKK(med3_i32, "v_med3_i32 %0, %0, %1, %1", seed)
+MKK(cndmask, "v_cndmask_b32 %0, %0, %1, vcc", seed)
+
+// 64-bit register (packed fp32) ops: instruction rate (each instruction = 2 fp32 lanes)
+#define MKK64(NAME, INSTR, INIT_B)                                                            \
+  __global__ void k_##NAME(uint32_t* out, uint32_t seed) {                                  \
+    uint64_t a0 = seed + threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 * 9,   \
+             a5 = a0 * 11, a6 = a0 * 13, a7 = a0 * 15, b = INIT_B;                          \
+    for (int i = 0; i < ITERS; ++i) {                                                        \
+      asm volatile(INSTR : "+v"(a0) : "v"(b)); asm volatile(INSTR : "+v"(a1) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a2) : "v"(b)); asm volatile(INSTR : "+v"(a3) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a4) : "v"(b)); asm volatile(INSTR : "+v"(a5) : "v"(b));      \
+      asm volatile(INSTR : "+v"(a6) : "v"(b)); asm volatile(INSTR : "+v"(a7) : "v"(b));      \
+    }                                                                                        \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+  }
+MKK64(pk_fma_f32, "v_pk_fma_f32 %0, %0, %1, %1", 0x3f0000003f000000ull)
+MKK64(pk_mul_f32, "v_pk_mul_f32 %0, %0, %1", 0x3f8000003f800000ull)
+MKK64(pk_add_f32, "v_pk_add_f32 %0, %0, %1", 0x3f0000003f000000ull)
 
 // Keccak-f[1600] on register state, PERMS permutations per lane
 __global__ __launch_bounds__(256) void k_keccak(uint64_t* out, int perms) {
@@ -140,7 +170,12 @@ int main() {
             {"mul_u32_u24", k_mul_u32_u24}, {"mul_hi_u32_u24", k_mul_hi_u32_u24}, {"mul_f32", k_mul_f32},
             {"fma_f32", k_fma_f32}, {"rndne_f32", k_rndne_f32}, {"dot2c_i32_i16", k_dot2c_i32_i16}, {"bcnt", k_bcnt},
             {"perm", k_perm}, {"bfe_u32", k_bfe_u32}, {"add_u32", k_add_u32}, {"lshl_add", k_lshl_add}, {"ashr", k_ashr},
-            {"pk_add_u16", k_pk_add_u16}, {"pk_mul_lo_u16", k_pk_mul_lo_u16}};
+            {"pk_add_u16", k_pk_add_u16}, {"pk_mul_lo_u16", k_pk_mul_lo_u16}, {"fmac_f32", k_fmac_f32},
+            {"fmaak_f32", k_fmaak_f32}, {"add_f32", k_add_f32}, {"cvt_f32_i32", k_cvt_f32_i32},
+            {"cvt_i32_f32", k_cvt_i32_f32}, {"mad_i32_i16", k_mad_i32_i16}, {"mad_u32_u16", k_mad_u32_u16},
+            {"mul_hi_i32", k_mul_hi_i32}, {"pk_mad_i16", k_pk_mad_i16}, {"sub_sdwa", k_sub_sdwa},
+            {"bfe_i32", k_bfe_i32}, {"med3_i32", k_med3_i32}, {"cndmask", k_cndmask},
+            {"pk_fma_f32_instr", k_pk_fma_f32}, {"pk_mul_f32_instr", k_pk_mul_f32}, {"pk_add_f32_instr", k_pk_add_f32}};
   for (auto& k : ks) {
     hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(threads), 0, 0, d, 1u);
     CHECK(hipDeviceSynchronize());
