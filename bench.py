@@ -256,6 +256,144 @@ def kernel_report(alg, mode, prof, B):
     return kernels, roof, mfma
 
 
+# ---------------------------------------------------------------- handshake mode
+SHA256_OPS = 1400  # VALU ops per SHA-256 compression (64 rounds x ~14 + 48-word schedule x ~10)
+
+
+def hkdf_compressions(ikm_len, info_len, key_len):
+    """HMAC-SHA256 extract + expand compressions for one key (hkdf.hip)."""
+    blocks = lambda n: (n + 9 + 63) // 64  # noqa: E731
+    extract = 1 + blocks(ikm_len) + 2
+    nt = -(-key_len // 32)
+    expand = 2 + sum(blocks((32 if r > 1 else 0) + info_len + 1) + 1 for r in range(1, nt + 1))
+    return extract + expand
+
+
+def mlkem_keygen_ops(alg):
+    k, eta1, _, _, _ = KP[alg]
+    pk, _, _ = mlkem_sizes(alg)
+    perms = 1 + 2 * k * (1 if eta1 == 2 else 2) + 3 * k * k + (pk + 1 + 135) // 136
+    return perms * PERM_OPS + 2 * k * 896 * 8 + k * k * 3584
+
+
+def handshake_ops(alg, info_len, key_len):
+    """Per handshake: 2 KeyGen + Encaps + Decaps + 2 HKDF (messaging.py:590, 809, 830, 845, 1038, 1068)."""
+    return 2 * mlkem_keygen_ops(alg) + valu_ops(alg, "encdec") + \
+        2 * hkdf_compressions(32, info_len, key_len) * SHA256_OPS
+
+
+def node_uuid(tag: str, i: int) -> str:
+    """UUID-formatted synthetic node id (the reference uses str(uuid.uuid4()),
+    networking/node_identity.py:78)."""
+    import hashlib
+    h = hashlib.sha256(f"{tag}{i}".encode()).hexdigest()
+    return f"{h[:8]}-{h[8:12]}-4{h[13:16]}-a{h[17:20]}-{h[20:32]}"
+
+
+def bench_handshake(args, world, rank, local):
+    """One step = N complete protocol key exchanges (qrk_handshake_batch) on device-resident
+    coins and per-handshake HKDF infos; value = handshakes/s."""
+    from qrkem.handshake import SYMMETRIC_KEY_SIZE, HandshakeDriver
+    from qrkem.shard import reduce_run, weak_shard
+    alg = args.alg
+    if alg not in KP:
+        raise SystemExit("handshake mode: ML-KEM algorithms only in the bench")
+    lb = args.log2_batch if args.log2_batch is not None else 20
+    B = 1 << lb
+    drv = HandshakeDriver(alg, symmetric_name=args.symmetric, device=local, chunk=args.chunk)
+    e = drv.engine
+    base = weak_shard(rank, world, B).first
+    kp, enc = e.kp_coins, e.enc_coins
+    coins = e.bench_coins(B, 2 * kp, args.seed, base)  # KeyGen coins (initiator | responder)
+    c_i, c_r = coins[:, :kp].contiguous(), coins[:, kp:].contiguous()
+    c_e = e.bench_coins(B, enc, args.seed ^ 0xE7C, base)  # Encaps coins: a second seed
+    del coins
+    # peer p talks to this server node: infos differ per handshake (sorted ids, messaging.py:364-367)
+    server = node_uuid("server-", rank)
+    infos = [drv.info_for(node_uuid("peer-", base + i), server) for i in range(B)]
+    info_len = sum(len(x) for x in infos) / B
+    packed = drv.pack(infos)
+
+    def step():
+        return drv.run(packed, coins_kp_initiator=c_i, coins_kp_responder=c_r, coins_encaps=c_e)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        e.profile(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = e.profile_read() if not args.no_profile else {}
+    e.profile(False)
+    disagree = int((out.agree != 1).sum().item())
+    elapsed, (disagree,) = reduce_run(elapsed, [disagree], device=f"cuda:{local}")
+    value = B * world * args.steps / elapsed
+    W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric])
+    k = KP[alg][0]
+    kernels, roof = {}, None
+    tot = sum(ms for ms, _ in prof.values()) or 1.0
+    for name, (ms, cnt) in prof.items():
+        kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot}
+    if "k_xof" in prof:  # 4 SampleNTT passes per handshake (2 KeyGen, Encaps, Decaps)
+        ms, cnt = prof["k_xof"]
+        ops = 4 * 3 * k * k * PERM_OPS * B * args.steps
+        roof = {"kernel": "k_xof", "bound": "valu", "achieved": ops / (ms * 1e-3) / 1e12,
+                "peak": VALU_PEAK / 1e12, "unit": "Top/s (int32 lane-ops)",
+                "frac": ops / (ms * 1e-3) / VALU_PEAK, "traffic": None, "avg_launch_ms": ms / cnt,
+                "algorithmic_ops_per_launch": ops / cnt}
+    result = {
+        "metric": f"{alg} protocol handshakes/sec at batch 2^{lb} per GPU "
+                  f"(2 KeyGen + Encaps + Decaps + 2 HKDF-SHA256)",
+        "value": value, "unit": "handshakes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic: coins = SHAKE256('qrk-bench'||LE64(seed)||LE64(i)) on device; UUID-formatted "
+                "node ids, per-handshake HKDF info (messaging.py:364-367)",
+        "config": {"workload": f"{alg} batched handshake driver, 2^{lb} exchanges per GPU (SURVEY.md 8f-1)",
+                   "alg": alg, "symmetric": args.symmetric, "batch_per_gpu": B, "global_batch": B * world,
+                   "mean_info_bytes": info_len, "parallelism": f"index-sharded x{world} (no data-path collective)"},
+        "roofline": roof, "valu_frac_of_peak_step": value * W / VALU_PEAK, "valu_ops_per_unit": W,
+        "kernels_timed_region": kernels, "checks": {"key_disagreements": disagree}, "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle as orc
+        threads = cpu_threads()
+        take = lambda t, n: np.ascontiguousarray(t[:n].cpu().numpy())  # noqa: E731
+        cal = 512
+        t0 = time.perf_counter()
+        orc.batch_handshake(alg, take(c_i, cal), take(c_r, cal), take(c_e, cal), infos[:cal], drv.key_len, threads)
+        rate = cal / (time.perf_counter() - t0)
+        S = int(min(B, max(cal, (rate * 12.0) // 256 * 256)))
+        t0 = time.perf_counter()
+        pk_i, pk_r, c, key_i, key_r = orc.batch_handshake(alg, take(c_i, S), take(c_r, S), take(c_e, S), infos[:S],
+                                                          drv.key_len, threads)
+        dt = time.perf_counter() - t0
+        match = all(np.array_equal(a, take(b, S)) for a, b in ((pk_i, out.pk_initiator), (pk_r, out.pk_responder),
+                                                                (c, out.ciphertext), (key_i, out.key_initiator),
+                                                                (key_r, out.key_responder)))
+        result["cpu_baseline"] = {
+            "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port",
+            "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so: FIPS 203 + RFC 5869 "
+                      f"C restatement, {threads} pthreads)",
+            "sample_matches_gpu": match}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,7 +403,8 @@ def main():
     ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM)")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
-    ap.add_argument("--mode", choices=["encdec", "decaps-tampered"], default="encdec")
+    ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake"], default="encdec")
+    ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -279,6 +418,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    if args.mode == "handshake":
+        return bench_handshake(args, world, rank, local)
     from qrkem.batch import BatchKEM
     from qrkem.shard import reduce_run, weak_shard
     alg = args.alg

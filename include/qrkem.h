@@ -149,6 +149,32 @@ int qrk_bench_coins(qrk_ctx *ctx, size_t n, size_t len, uint64_t seed, uint64_t 
  * h_i = SHAKE256("qrk-tamper"||LE64(seed)||LE64(i))[0..8), bit (h_i>>1) mod 8*ctlen. */
 int qrk_tamper(qrk_ctx *ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t *ct, void *stream);
 
+/* HKDF-SHA256 (RFC 5869) over n keys, one GPU lane per key.  Replaces
+ * SecureMessaging._derive_symmetric_key (messaging.py:350-382: HKDF(SHA256,
+ * length=key_size, salt=None, info=...).derive(shared_secret)).
+ * Device pointers: ikm [n][ikm_len]; salt [salt_len] shared by all keys (NULL/0 =
+ * HashLen zero bytes, as salt=None); okm [n][okm_len], 1 <= okm_len <= 8160.
+ * info: with info_off (device uint64[n+1]) key i uses info[info_off[i] .. info_off[i+1]);
+ * with info_off NULL every key uses info[0 .. info_len). */
+int qrk_hkdf_sha256_batch(qrk_ctx *ctx, size_t n, const uint8_t *ikm, size_t ikm_len, const uint8_t *salt,
+                          size_t salt_len, const uint8_t *info, const uint64_t *info_off, size_t info_len,
+                          uint8_t *okm, size_t okm_len, void *stream);
+
+/* n complete protocol key exchanges with the reference's per-handshake operation mix
+ * (messaging.py:546-1146): initiator KeyGen (:590); responder KeyGen (:809, its pk is
+ * sent back at :853), Encaps of the initiator's pk (:830) and HKDF (:845); initiator
+ * Decaps (:1038) and HKDF (:1068).  Device pointers.  Coins (each nullable = OS CSPRNG):
+ * coins_kp_i / coins_kp_r [n][keypair coin bytes], coins_enc [n][encaps coin bytes].
+ * info / info_off / info_len as qrk_hkdf_sha256_batch (salt = None).  Outputs (the wire
+ * and the keys): pk_i, pk_r [n][pk], ct [n][ct], key_i, key_r [n][key_len]; agree
+ * (nullable, int32[n]) = 1 where both sides derived the same key.  Ephemeral secret keys
+ * and shared secrets stay in context scratch and are zeroed before the call returns
+ * (stream-ordered). */
+int qrk_handshake_batch(qrk_ctx *ctx, const char *alg, size_t n, const uint8_t *coins_kp_i,
+                        const uint8_t *coins_kp_r, const uint8_t *coins_enc, const uint8_t *info,
+                        const uint64_t *info_off, size_t info_len, size_t key_len, uint8_t *pk_i, uint8_t *pk_r,
+                        uint8_t *ct, uint8_t *key_i, uint8_t *key_r, int32_t *agree, void *stream);
+
 /* Per-kernel HIP-event timing on the launch stream (for bench.py's roofline).
  * qrk_ctx_profile(ctx, 1) resets and enables; qrk_ctx_profile_collect()
  * synchronises the recorded events and returns the number of distinct kernel

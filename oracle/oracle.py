@@ -165,3 +165,74 @@ def aes_block(key: bytes, block: bytes) -> bytes:
     out = ct.create_string_buffer(16)
     lib().orc_aes(_buf(key), 8 * len(key), _buf(block), out)
     return out.raw
+
+
+# ---------------------------------------------------------------- HKDF-SHA256 / handshake
+def _hk():
+    L = lib()
+    if not getattr(L, "_hk_bound", False):
+        P, SZ = ct.c_void_p, ct.c_size_t
+        L.orc_sha256.argtypes = [P, P, SZ]
+        L.orc_sha256.restype = None
+        L.orc_hkdf_sha256.argtypes = [P, SZ, P, SZ, P, SZ, P, SZ]
+        L.orc_hkdf_batch.argtypes = [SZ, ct.c_int, P, SZ, P, SZ, P, P, SZ, P, SZ]
+        L.orc_handshake_batch.argtypes = [ct.c_char_p, SZ, ct.c_int, P, P, P, P, P, SZ, SZ, P, P, P, P, P]
+        L._hk_bound = True
+    return L
+
+
+def sha256(data: bytes) -> bytes:
+    out = ct.create_string_buffer(32)
+    _hk().orc_sha256(out, _buf(data), len(data))
+    return out.raw
+
+
+def hkdf_sha256(ikm: bytes, info: bytes, length: int, salt: bytes | None = None) -> bytes:
+    out = ct.create_string_buffer(max(length, 1))
+    rc = _hk().orc_hkdf_sha256(out, length, _buf(ikm), len(ikm), _buf(salt) if salt else None,
+                               len(salt) if salt else 0, _buf(info), len(info))
+    if rc:
+        raise ValueError("bad HKDF length")
+    return out.raw[:length]
+
+
+def pack_infos(infos) -> tuple[np.ndarray, np.ndarray]:
+    """list[bytes] -> (concatenated uint8, uint64 offsets [n+1])."""
+    off = np.zeros(len(infos) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in infos])
+    data = np.frombuffer(b"".join(infos) or b"\0", np.uint8).copy()
+    return data, off
+
+
+def batch_hkdf(ikm: np.ndarray, infos, length: int, salt: bytes | None = None, threads: int = 0) -> np.ndarray:
+    n = ikm.shape[0]
+    data, off = pack_infos(infos)
+    okm = np.zeros((n, length), np.uint8)
+    ikm = np.ascontiguousarray(ikm)
+    rc = _hk().orc_hkdf_batch(n, threads or os.cpu_count(), _ptr(ikm), ikm.shape[1],
+                              _buf(salt) if salt else None, len(salt) if salt else 0,
+                              _ptr(data), _ptr(off), 0, _ptr(okm), length)
+    if rc:
+        raise RuntimeError("oracle batch hkdf failed")
+    return okm
+
+
+def batch_handshake(alg: str, coins_kp_i: np.ndarray, coins_kp_r: np.ndarray, coins_enc: np.ndarray,
+                    infos, key_len: int, threads: int = 0):
+    """Per handshake: KeyGen_i, KeyGen_r, Encaps(pk_i), HKDF, Decaps(sk_i, ct), HKDF
+    (messaging.py:590, 809, 830, 845, 1038, 1068).  Returns pk_i, pk_r, ct, key_i, key_r."""
+    s = sizes(alg)
+    n = coins_kp_i.shape[0]
+    data, off = pack_infos(infos)
+    pk_i = np.zeros((n, s["pk"]), np.uint8)
+    pk_r = np.zeros((n, s["pk"]), np.uint8)
+    c = np.zeros((n, s["ct"]), np.uint8)
+    key_i = np.zeros((n, key_len), np.uint8)
+    key_r = np.zeros((n, key_len), np.uint8)
+    args = [np.ascontiguousarray(x) for x in (coins_kp_i, coins_kp_r, coins_enc)]
+    rc = _hk().orc_handshake_batch(alg.encode(), n, threads or os.cpu_count(), *[_ptr(x) for x in args],
+                                   _ptr(data), _ptr(off), 0, key_len, _ptr(pk_i), _ptr(pk_r), _ptr(c),
+                                   _ptr(key_i), _ptr(key_r))
+    if rc:
+        raise RuntimeError("oracle batch handshake failed")
+    return pk_i, pk_r, c, key_i, key_r

@@ -125,6 +125,8 @@ struct qrk_ctx {
   size_t hstage_bytes = 0;
   hipStream_t aux = nullptr;  // side stream for independent kernel chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  uint8_t* hs_scratch = nullptr;  // handshake driver: ephemeral sk / ss of one chunk
+  size_t hs_scratch_bytes = 0;
   int streams = 2;            // 1: serial schedule (kernel timings in isolation), 2: forked
   std::mutex mu;
 };
@@ -203,6 +205,13 @@ static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
   return cap;
 }
 
+// Routes QRK_LAUNCH timing to the context's timer for the scope's lifetime (nests).
+struct TimerScope {
+  KernelTimer* prev;
+  explicit TimerScope(KernelTimer* t) : prev(g_timer) { g_timer = t; }
+  ~TimerScope() { g_timer = prev; }
+};
+
 // Core batched driver over device pointers, chunked.
 static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
                      const uint8_t* i2, int32_t* status, hipStream_t st) {
@@ -239,10 +248,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   S.aux = ctx->streams > 1 ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
-  struct TimerScope {
-    explicit TimerScope(KernelTimer* t) { g_timer = t; }
-    ~TimerScope() { g_timer = nullptr; }
-  } timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     hipError_t e = hipSuccess;
@@ -487,6 +493,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
     (void)hipDeviceSynchronize();
   }
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->hs_scratch) (void)hipFree(ctx->hs_scratch);
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
@@ -610,6 +617,71 @@ int qrk_tamper(qrk_ctx* ctx, size_t n, size_t ctlen, uint64_t seed, int mode, ui
   if (ensure_device(ctx->device)) return -1;
   hipError_t e = tamper_ciphertexts(n, ctlen, seed, mode, ct, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail("tamper", e);
+}
+
+int qrk_hkdf_sha256_batch(qrk_ctx* ctx, size_t n, const uint8_t* ikm, size_t ikm_len, const uint8_t* salt,
+                          size_t salt_len, const uint8_t* info, const uint64_t* info_off, size_t info_len,
+                          uint8_t* okm, size_t okm_len, void* stream) {
+  if (!ctx) return fail("null context");
+  if (okm_len == 0 || okm_len > 255 * 32) return fail("HKDF-SHA256 output length must be 1..8160 bytes");
+  if (salt_len && !salt) return fail("salt_len > 0 with a NULL salt");
+  if (n && (!ikm || !okm || (!info && (info_off || info_len)))) return fail("null buffer");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (ensure_device(ctx->device)) return -1;
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  hipError_t e = hkdf_sha256(n, ikm, ikm_len, ikm_len, salt, salt_len, info, info_off, info_len, okm_len, okm,
+                             okm_len, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("hkdf_sha256", e);
+}
+
+int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* coins_kp_i,
+                        const uint8_t* coins_kp_r, const uint8_t* coins_enc, const uint8_t* info,
+                        const uint64_t* info_off, size_t info_len, size_t key_len, uint8_t* pk_i, uint8_t* pk_r,
+                        uint8_t* ct, uint8_t* key_i, uint8_t* key_r, int32_t* agree, void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  if (key_len == 0 || key_len > 255 * 32) return fail("key_len must be 1..8160 bytes");
+  if (n == 0) return 0;
+  if (!pk_i || !pk_r || !ct || !key_i || !key_r) return fail("null output buffer");
+  if (ensure_device(ctx->device)) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  // Ephemeral secrets of one chunk live in context scratch and are wiped afterwards
+  // (the reference keeps them in Python objects: messaging.py:590-600, 809).
+  const size_t chunk = chunk_for(ctx, *a);
+  const size_t m0 = std::min(chunk, n);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_sk = al(m0 * a->sk), b_ss = al(m0 * a->ss);
+  if (grow_device((void**)&ctx->hs_scratch, &ctx->hs_scratch_bytes, 2 * b_sk + 2 * b_ss, st)) return -1;
+  uint8_t *sk_i = ctx->hs_scratch, *sk_r = sk_i + b_sk, *ss_i = sk_r + b_sk, *ss_r = ss_i + b_ss;
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t m = std::min(chunk, n - off);
+    auto co = [&](const uint8_t* c, size_t len) { return c ? c + off * len : nullptr; };
+    // initiate_key_exchange: ephemeral KeyGen (messaging.py:590)
+    if (run_batch(ctx, *a, Op::KEYPAIR, m, pk_i + off * a->pk, sk_i, co(coins_kp_i, a->kp_coins), nullptr, nullptr,
+                  st))
+      return -1;
+    // _handle_key_exchange_init: responder KeyGen (:809, pk sent back at :853) + Encaps (:830)
+    if (run_batch(ctx, *a, Op::KEYPAIR, m, pk_r + off * a->pk, sk_r, co(coins_kp_r, a->kp_coins), nullptr, nullptr,
+                  st))
+      return -1;
+    if (run_batch(ctx, *a, Op::ENCAPS, m, ct + off * a->ct, ss_r, pk_i + off * a->pk, co(coins_enc, a->enc_coins),
+                  nullptr, st))
+      return -1;
+    hipError_t e = hkdf_sha256(m, ss_r, a->ss, a->ss, nullptr, 0, info, info_off ? info_off + off : nullptr,
+                               info_len, key_len, key_r + off * key_len, key_len, st);  // :845
+    if (e != hipSuccess) return hip_fail("hkdf_sha256", e);
+    // _handle_key_exchange_response: Decaps (:1038) + HKDF (:1068)
+    if (run_batch(ctx, *a, Op::DECAPS, m, ss_i, nullptr, ct + off * a->ct, sk_i, nullptr, st)) return -1;
+    e = hkdf_sha256(m, ss_i, a->ss, a->ss, nullptr, 0, info, info_off ? info_off + off : nullptr, info_len,
+                    key_len, key_i + off * key_len, key_len, st);
+    if (e != hipSuccess) return hip_fail("hkdf_sha256", e);
+    if (agree) {
+      e = keys_equal(m, key_i + off * key_len, key_r + off * key_len, key_len, agree + off, st);
+      if (e != hipSuccess) return hip_fail("keys_equal", e);
+    }
+  }
+  hipError_t e = hipMemsetAsync(ctx->hs_scratch, 0, 2 * b_sk + 2 * b_ss, st);
+  return e == hipSuccess ? 0 : hip_fail("hipMemsetAsync(cleanse)", e);
 }
 
 const char* qrk_last_error(void) { return g_err.c_str(); }

@@ -82,4 +82,12 @@ hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint
 // (bench config 5).  mode: 0 none, 1 all, 2 mixed.
 hipError_t tamper_ciphertexts(size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t* ct, hipStream_t st);
 
+// HKDF-SHA256 (RFC 5869), one lane per key (hkdf.hip).  info_off (n+1 offsets) may be
+// NULL, then every key uses info[0 .. info_len).  L <= 8160.
+hipError_t hkdf_sha256(size_t n, const uint8_t* ikm, size_t ikm_len, size_t ikm_stride, const uint8_t* salt,
+                       size_t salt_len, const uint8_t* info, const uint64_t* info_off, size_t info_len, size_t L,
+                       uint8_t* okm, size_t okm_stride, hipStream_t st);
+// agree_i = (a_i == b_i), len bytes each
+hipError_t keys_equal(size_t n, const uint8_t* a, const uint8_t* b, size_t len, int32_t* agree, hipStream_t st);
+
 }  // namespace qrk

@@ -9,7 +9,7 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
-for p in (ROOT / "quantum-resistant-p2p_amd", ROOT / "oracle", ROOT / "oracle" / "py", ROOT):
+for p in (ROOT / "quantum-resistant-p2p_amd", ROOT / "oracle", ROOT / "oracle" / "py", ROOT / "tests" / "golden", ROOT):
     if str(p) not in sys.path:
         sys.path.insert(0, str(p))
 
