@@ -83,7 +83,13 @@ def valu_ops_encdec(alg) -> int:
 
 # FrodoKEM (n, logq, sec, hash rate bytes): FrodoKEM spec round 3 / SURVEY.md 8a A18-A21
 FP = {"FrodoKEM-640-SHAKE": (640, 15, 16, 168), "FrodoKEM-976-SHAKE": (976, 16, 24, 136),
-      "FrodoKEM-1344-SHAKE": (1344, 16, 32, 136)}
+      "FrodoKEM-1344-SHAKE": (1344, 16, 32, 136), "FrodoKEM-640-AES": (640, 15, 16, 168),
+      "FrodoKEM-976-AES": (976, 16, 24, 136), "FrodoKEM-1344-AES": (1344, 16, 32, 136)}
+# AES Gen(A): FIPS-minimal T-table AES-128 = 10 rounds x 16 table lookups per 16-byte block;
+# one ds_read_b32 wave instruction takes 2 LDS cycles (MI355X_MICROARCH.md LDS table) ->
+# 32 lookups per clock per CU
+AES_LOOKUPS_PER_BLOCK = 160
+LDS_LOOKUP_PEAK = 256 * 32 * 2.4e9
 MFMA_I8_PEAK = 5.0e15  # dense int8 MFMA ops/s (MI355X_MICROARCH.md: I8 = 2x BF16 per clock, BF16 ~2.5 PF dense)
 
 
@@ -98,7 +104,7 @@ def frodo_perms(alg):
     n, logq, sec, rate = FP[alg]
     pk, _, ct = frodo_sizes(alg)
     se_words = (2 * n + 8) * 8 * 2 // 8
-    gen_a = n * -(-2 * n // 168)                       # SHAKE128 rows of A
+    gen_a = 0 if alg.endswith("-AES") else n * -(-2 * n // 168)  # SHAKE128 rows of A
     se = -(-se_words * 8 // rate)                      # SHAKE(0x96 || seedSE) stream
     ss = -(-(ct + sec + 1) // rate)                    # ss = H(ct || k)
     return {"k_fr_gen_at": gen_a, "k_fr_se_stream": se, "k_fr_ss": ss,
@@ -114,6 +120,8 @@ def kernel_ops_per_hs(alg, name, mode):
         perms = frodo_perms(alg)
         if name == "k_fr_gen_mm":  # Gen(A) Keccak (the bound) fused with S'A on MFMA
             return calls * perms["k_fr_gen_at"] * PERM_OPS, "valu"
+        if name == "k_fr_gen_mm_aes":  # Gen(A) AES-128 T-table lookups (LDS) fused with S'A on MFMA
+            return calls * n * (n // 8) * AES_LOOKUPS_PER_BLOCK, "lds"
         if name in ("k_fr_front_enc",):
             return (perms[name] * PERM_OPS if mode == "encdec" else None), "valu"
         if name in perms:
@@ -225,7 +233,7 @@ def kernel_report(alg, mode, prof, B):
         kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot_ms}
         if ops is not None:
             rate = ops * B / (ms * 1e-3)
-            peak = MFMA_I8_PEAK if bound == "mfma" else VALU_PEAK
+            peak = {"mfma": MFMA_I8_PEAK, "lds": LDS_LOOKUP_PEAK}.get(bound, VALU_PEAK)
             kernels[name].update(bound=bound, achieved_Tops=rate / 1e12, frac=rate / peak)
     roof, mfma = None, None
     if prof:
@@ -234,25 +242,30 @@ def kernel_report(alg, mode, prof, B):
         ms, cnt = prof[dom]
         if ops is not None:
             achieved = ops * B / (ms * 1e-3)
-            peak = MFMA_I8_PEAK if bound == "mfma" else VALU_PEAK
+            peak = {"mfma": MFMA_I8_PEAK, "lds": LDS_LOOKUP_PEAK}.get(bound, VALU_PEAK)
             roof = {"kernel": dom, "bound": bound, "achieved": achieved / 1e12, "peak": peak / 1e12,
-                    "unit": "Top/s (int32 lane-ops)" if bound == "valu" else "Top/s (int8 MFMA ops)",
+                    "unit": {"valu": "Top/s (int32 lane-ops)", "lds": "T lookups/s (LDS ds_read_b32 lanes)"}.get(
+                        bound, "Top/s (int8 MFMA ops)"),
                     "frac": achieved / peak, "traffic": None,
                     "ops_per_launch": ops * B / cnt, "avg_launch_ms": ms / cnt}
-        if "k_fr_gen_mm" in prof:
+        gk = "k_fr_gen_mm_aes" if "k_fr_gen_mm_aes" in prof else "k_fr_gen_mm"
+        if gk in prof:
             # S'A runs on MFMA inside the fused Gen(A) kernel: its rate is priced over that
             # kernel's whole duration (a lower bound on the MFMA pipe's own utilisation)
             n = FP[alg][0]
             calls = 2 if mode == "encdec" else 1
-            ms, cnt = prof["k_fr_gen_mm"]
-            tiles = sum(-(-min(84, n - 84 * b) // 16) for b in range(-(-2 * n // 168)))
+            ms, cnt = prof[gk]
+            if gk == "k_fr_gen_mm_aes":
+                tiles = n // 16
+            else:
+                tiles = sum(-(-min(84, n - 84 * b) // 16) for b in range(-(-2 * n // 168)))
             alg_ops = calls * 2 * 2 * 8 * n * n * B
             issued = calls * (-(-n // 64)) * tiles * 2 * (16 * 16 * 64 * 2) * B
-            mfma = {"kernel": "k_fr_gen_mm (S'A fused into Gen(A))", "achieved": alg_ops / (ms * 1e-3) / 1e12,
+            mfma = {"kernel": f"{gk} (S'A fused into Gen(A))", "achieved": alg_ops / (ms * 1e-3) / 1e12,
                     "issued": issued / (ms * 1e-3) / 1e12, "peak": MFMA_I8_PEAK / 1e12,
                     "unit": "Top/s (int8 MFMA ops; algorithmic = 2 limbs x 2 x 8 x n^2 per S'A)",
                     "frac": alg_ops / (ms * 1e-3) / MFMA_I8_PEAK, "avg_launch_ms": ms / cnt,
-                    "note": "MFMA is not the bound: Keccak (Gen(A)) is; see roofline"}
+                    "note": "MFMA is not the bound: Gen(A) (Keccak or AES) is; see roofline"}
     return kernels, roof, mfma
 
 
@@ -550,7 +563,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32" if not frodo else "u32 (Keccak) + i8->i32 (MFMA)",
+        "dtype": "u32" if not frodo else ("u32 (AES T-table) + i8->i32 (MFMA)" if alg.endswith("-AES") else "u32 (Keccak) + i8->i32 (MFMA)"),
         "data": "synthetic: coins = SHAKE256('qrk-bench'||LE64(seed)||LE64(i)) generated on device; "
                 "keys from batched KeyGen on those coins",
         "config": {"workload": f"{alg} {what} of 2^{lb} device-resident handshakes per GPU "

@@ -26,11 +26,11 @@ static AlgInfo ALGS[] = {
     {"ML-KEM-512", Family::MLKEM, 1, 2, 800, 1632, 768, 32, 64, 32, false, true},
     {"ML-KEM-768", Family::MLKEM, 3, 3, 1184, 2400, 1088, 32, 64, 32, false, true},
     {"ML-KEM-1024", Family::MLKEM, 5, 4, 1568, 3168, 1568, 32, 64, 32, false, true},
-    {"FrodoKEM-640-AES", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, true, false},
+    {"FrodoKEM-640-AES", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, true, true},
     {"FrodoKEM-640-SHAKE", Family::FRODO, 1, 640, 9616, 19888, 9720, 16, 48, 16, false, true},
-    {"FrodoKEM-976-AES", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, true, false},
+    {"FrodoKEM-976-AES", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, true, true},
     {"FrodoKEM-976-SHAKE", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, false, true},
-    {"FrodoKEM-1344-AES", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, true, false},
+    {"FrodoKEM-1344-AES", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, true, true},
     {"FrodoKEM-1344-SHAKE", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, false, true},
 };
 static const int NALG = (int)(sizeof(ALGS) / sizeof(ALGS[0]));

@@ -25,6 +25,7 @@
 //   k_fr_ss           lane / hs   ss = H(ct || k)
 // KeyGen: k_fr_kg_front (seedA, SHAKE(0x5F || seedSE) stream), k_fr_sample,
 // k_fr_kg_rows (lane / row: Gen(A) row and B = AS + E on VALU), k_fr_kg_pack.
+#include "aes.cuh"
 #include "keccak.cuh"
 #include "qrkem_internal.h"
 
@@ -90,6 +91,7 @@ struct View {
   uint16_t* part;  // per-wave partial S'A (u16, mod 2^16) [C][NWV][8][N]; KeyGen: B [C][N][8]
   uint64_t* seeds; // per hs 16 u64: seedSE | k | pkh | mu'  (4 x 32 B)
   uint64_t* kk;    // per hs 4 u64: key fed to the final hash
+  uint32_t* aesp;  // FrodoKEM-AES: per hs aes::prep_words<N>() words (round keys, round-2 parts)
 };
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -99,7 +101,7 @@ size_t scratch_bytes_t(size_t C) {
   using P = FP<N>;
   const size_t W = (size_t)(P::SE_WORDS > P::KG_WORDS ? P::SE_WORDS : P::KG_WORDS);
   return al256(C * W * 8) + al256(C * 8 * P::NP) + al256(C * 8 * N * 2) + al256(C * 64 * 2) +
-         al256(C * P::NWV * 8 * N * 2) + al256(C * 128) + al256(C * 32);
+         al256(C * P::NWV * 8 * N * 2) + al256(C * 128) + al256(C * 32) + al256(C * aes::prep_words<N>() * 4);
 }
 
 template <int N>
@@ -121,6 +123,8 @@ View<N> carve(void* base, size_t C) {
   v.seeds = (uint64_t*)p;
   p += al256(C * 128);
   v.kk = (uint64_t*)p;
+  p += al256(C * 32);
+  v.aesp = (uint32_t*)p;
   return v;
 }
 
@@ -342,6 +346,146 @@ __global__ __launch_bounds__(64) void k_fr_gen_mm(const uint8_t* __restrict__ se
         const v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, y, z, 0, 0, 0);
         const int cl = 16 * t + 4 * (lane >> 4);
         if (kq < NBAR && cl < nc) {
+          uint32_t v[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)dl[g] + ((uint32_t)dh[g] << 8)) & 0xFFFFu;
+          *(uint2*)(prt + kq * N + c0 + cl) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// ---------------------------------------------------------------- FrodoKEM-AES Gen(A)
+// Per handshake (lane per (hs, column block jb)): round keys of seedA, the round-1
+// constants and the uniform round-2 part of column block jb (aes.cuh).  seedA at
+// seed_base + hs * seed_stride (pk, or the pk copy inside sk).
+template <int N>
+__global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__ seed_base, size_t seed_stride,
+                                                     size_t n, uint32_t* __restrict__ prep) {
+  using namespace aes;
+  constexpr int NB = N / 8, W = prep_words<N>();
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t hs = t / NB;
+  const int jb = (int)(t % NB);
+  if (hs >= n) return;
+  const uint32_t* sa = (const uint32_t*)(seed_base + hs * seed_stride);
+  const uint32_t key[4] = {sa[0], sa[1], sa[2], sa[3]};
+  uint32_t rk[44];
+  expand_key(key, rk);
+  const uint32_t r1 = rk[1], r2 = rk[2], r3 = rk[3];
+  // round-1 output columns with the (i, j)-dependent byte left out (see aes.cuh)
+  const uint32_t C0 = Tg(1, B(r1, 1)) ^ Tg(2, B(r2, 2)) ^ Tg(3, B(r3, 3)) ^ rk[4];
+  const uint32_t C1 = Tg(0, B(r1, 0)) ^ Tg(1, B(r2, 1)) ^ Tg(2, B(r3, 2)) ^ rk[5];
+  const uint32_t C2 = Tg(0, B(r2, 0)) ^ Tg(1, B(r3, 1)) ^ Tg(3, B(r1, 3)) ^ rk[6];
+  const uint32_t C3 = Tg(0, B(r3, 0)) ^ Tg(2, B(r1, 2)) ^ Tg(3, B(r2, 3)) ^ rk[7];
+  uint32_t* o = prep + hs * W;
+  if (jb == 0) {
+#pragma unroll
+    for (int i = 0; i < 44; ++i) o[i] = rk[i];
+    o[44] = C0, o[45] = C3, o[46] = C1, o[47] = C2;
+  }
+  const uint32_t j = 8u * (uint32_t)jb, k = rk[0];
+  const uint32_t y1 = Tg(3, ((j >> 8) ^ (k >> 24)) & 0xFF) ^ C1;  // column 1 after round 1
+  const uint32_t y2 = Tg(2, (j ^ (k >> 16)) & 0xFF) ^ C2;         // column 2 after round 1
+  uint32_t* u = o + PREP_HDR + 4 * jb;
+  u[0] = Tg(1, B(y1, 1)) ^ Tg(2, B(y2, 2)) ^ rk[8];
+  u[1] = Tg(0, B(y1, 0)) ^ Tg(1, B(y2, 1)) ^ rk[9];
+  u[2] = Tg(0, B(y2, 0)) ^ Tg(3, B(y1, 3)) ^ rk[10];
+  u[3] = Tg(2, B(y1, 2)) ^ Tg(3, B(y2, 3)) ^ rk[11];
+}
+
+// Gen(A) with AES-128 fused with S'A on i8 MFMA.  Same contraction as k_fr_gen_mm (one
+// wave = 64 consecutive rows of one handshake, lane = row, per-wave u16 partial sums of
+// S'A), but the 512-thread workgroup's 8 waves share one LDS-replicated T-table, and A is
+// produced 16 columns (two interleaved AES blocks) per MFMA stage.
+#ifndef QRK_AES_WAVES
+#define QRK_AES_WAVES 8
+#endif
+#ifndef QRK_AES_COLS
+#define QRK_AES_COLS 16
+#endif
+#ifndef QRK_AES_T2
+#define QRK_AES_T2 0
+#endif
+constexpr int AES_WAVES = QRK_AES_WAVES;
+constexpr int AES_COLS = QRK_AES_COLS;
+template <int N>
+__global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t* __restrict__ prep, size_t n,
+                                                       const int8_t* __restrict__ sp8, uint16_t* __restrict__ part) {
+  using P = FP<N>;
+  static_assert(N % 16 == 0 && AES_COLS % 16 == 0, "MFMA stages assume whole 16-column tiles (block pairs)");
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
+#if QRK_AES_T2
+  __shared__ __attribute__((aligned(16))) uint32_t tab2[256 * 32];
+  aes::fill_lds2(tab, tab2, threadIdx.x, 64 * AES_WAVES);
+#else
+  aes::fill_lds(tab, threadIdx.x, 64 * AES_WAVES);
+#endif
+  __shared__ __attribute__((aligned(16))) uint16_t stg[AES_WAVES][AES_COLS * ST_PITCH];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t item = (uint32_t)blockIdx.x * AES_WAVES + (uint32_t)wave;
+  if (item >= (uint32_t)(n * P::NWV)) return;
+  const uint32_t hs = __builtin_amdgcn_readfirstlane(item / P::NWV);
+  const int wv = (int)__builtin_amdgcn_readfirstlane(item % P::NWV);
+  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
+#if QRK_AES_T2
+  const aes::Lds2 L{(const char*)tab, (const char*)tab2, (uint32_t)(lane & 31) * 4u};
+#else
+  const aes::Lds L{(const char*)tab, (uint32_t)(lane & 31) * 4u};
+#endif
+  const int r = wv * 64 + lane;
+  const int kq = lane & 15, ks = 16 * (lane >> 4);
+  v4i y = {0, 0, 0, 0};
+  if (kq < NBAR) y = *(const v4i*)(sp8 + ((size_t)hs * NBAR + kq) * P::NP + wv * 64 + ks);  // zero past row N
+  uint32_t lp[4];
+  aes::row_part(L, hp, (uint32_t)r, lp);
+  uint16_t* st = stg[wave];
+  uint16_t* prt = part + ((size_t)hs * P::NWV + wv) * NBAR * N;
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += AES_COLS) {
+    const int nc = (N - c0) < AES_COLS ? (N - c0) : AES_COLS;
+#pragma unroll
+    for (int b = 0; b < AES_COLS / 8; b += 2) {  // pairs of AES blocks (N / 8 is even)
+      if (8 * b < nc) {
+        const uint32_t* u = hp + aes::PREP_HDR + 4 * ((c0 >> 3) + b);
+        uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
+        uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
+        aes::rounds_3_10_x2(L, z, w, hp);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {  // word q = values 2q, 2q+1 (little-endian u16)
+          const uint32_t x = q < 4 ? z[q] : w[q - 4];
+          const uint32_t al = __builtin_amdgcn_perm(add80(x), x, 0x07020500u);
+          st[(8 * b + 2 * q) * ST_PITCH + lane] = (uint16_t)al;
+          st[(8 * b + 2 * q + 1) * ST_PITCH + lane] = (uint16_t)(al >> 16);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int t = 0; t < AES_COLS / 16; ++t) {
+      if (16 * t < nc) {
+        const uint16_t* src = st + (16 * t + kq) * ST_PITCH + ks;
+        const uint4 a0 = *(const uint4*)src;
+        const uint4 a1 = *(const uint4*)(src + 8);
+        const uint32_t w8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        v4i xl, xh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xl[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x06040200u);
+          xh[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x07050301u);
+        }
+        const v4i zr = {0, 0, 0, 0};
+        const v4i dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, y, zr, 0, 0, 0);
+        const v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, y, zr, 0, 0, 0);
+        const int cl = 16 * t + 4 * (lane >> 4);
+        if (kq < NBAR) {
           uint32_t v[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)dl[g] + ((uint32_t)dh[g] << 8)) & 0xFFFFu;
@@ -664,6 +808,46 @@ __global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ 
   for (int k = 0; k < NBAR; ++k) bmat[(hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
 }
 
+// FrodoKEM-AES KeyGen rows: B = A S + E on VALU, lane = row, A from AES-128 (aes.cuh),
+// 256-thread workgroups sharing the LDS T-table and S^T.  KeyGen is not on the timed path.
+template <int N>
+__global__ __launch_bounds__(256) void k_fr_kg_rows_aes(const uint32_t* __restrict__ prep, size_t n,
+                                                        const int8_t* __restrict__ sp8,
+                                                        const int16_t* __restrict__ e16, uint16_t* __restrict__ bmat) {
+  using P = FP<N>;
+  constexpr int WGS_PER_HS = (N + 255) / 256;
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
+  __shared__ int8_t st[NBAR * P::NP];
+  const uint32_t hs = __builtin_amdgcn_readfirstlane(blockIdx.x / WGS_PER_HS);
+  if (hs >= n) return;
+  const int r = (int)(blockIdx.x % WGS_PER_HS) * 256 + threadIdx.x;
+  aes::fill_lds(tab, threadIdx.x, 256);
+  for (int t = threadIdx.x; t < NBAR * P::NP; t += 256) st[t] = sp8[(size_t)hs * NBAR * P::NP + t];
+  __syncthreads();
+  if (r >= N) return;
+  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
+  const aes::Lds L{(const char*)tab, (uint32_t)(threadIdx.x & 31) * 4u};
+  uint32_t lp[4];
+  aes::row_part(L, hp, (uint32_t)r, lp);
+  uint32_t acc[NBAR];
+#pragma unroll
+  for (int k = 0; k < NBAR; ++k) acc[k] = (uint32_t)(int32_t)e16[((size_t)hs * N + r) * NBAR + k];
+#pragma unroll 1
+  for (int jb = 0; jb < N / 8; ++jb) {
+    const uint32_t* u = hp + aes::PREP_HDR + 4 * jb;
+    uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
+    aes::rounds_3_10(L, z, hp);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t v = (z[e >> 1] >> (16 * (e & 1))) & 0xFFFF;
+#pragma unroll
+      for (int k = 0; k < NBAR; ++k) acc[k] += v * (uint32_t)(int32_t)st[k * P::NP + 8 * jb + e];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NBAR; ++k) bmat[((size_t)hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
+}
+
 // pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh.  One 256-thread workgroup
 // per handshake; packed B is staged in LDS and copied out with 8-byte stores (pkh is hashed
 // by k_fr_kg_pkh afterwards; seedA and s were written by k_fr_kg_front).
@@ -730,14 +914,21 @@ inline unsigned blocks_for(size_t t, int per = 256) { return (unsigned)((t + per
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
 // per-wave partial sums of S'A for every handshake of the chunk (Gen(A) fused)
-template <int N>
+template <int N, bool AES>
 void launch_sa(const View<N>& v, const uint8_t* seed_base, size_t seed_stride, size_t n, hipStream_t st) {
   using P = FP<N>;
-  QRK_LAUNCH("k_fr_gen_mm", st, k_fr_gen_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, seed_base, seed_stride,
-             n, v.sp8, v.part);
+  if constexpr (AES) {
+    QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, seed_base,
+               seed_stride, n, v.aesp);
+    QRK_LAUNCH("k_fr_gen_mm_aes", st, k_fr_gen_mm_aes<N>, dim3(blocks_for(n * P::NWV, AES_WAVES)),
+               dim3(64 * AES_WAVES), 0, st, v.aesp, n, v.sp8, v.part);
+  } else {
+    QRK_LAUNCH("k_fr_gen_mm", st, k_fr_gen_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, seed_base,
+               seed_stride, n, v.sp8, v.part);
+  }
 }
 
-template <int N>
+template <int N, bool AES>
 hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* mu, void* scratch,
                     hipStream_t st) {
   using P = FP<N>;
@@ -748,14 +939,14 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
              P::SE_WORDS, P::SE_WORDS, v.raw);
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
-  launch_sa<N>(v, pk, P::PK, n, st);
+  launch_sa<N, AES>(v, pk, P::PK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
              v.ep16, v.epp16, v.part, v.seeds, mu, (size_t)P::MU, ct, nullptr, nullptr, (size_t)0, v.kk);
   QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
   return hipGetLastError();
 }
 
-template <int N>
+template <int N, bool AES>
 hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch, hipStream_t st) {
   using P = FP<N>;
   const size_t C = round64(n);
@@ -767,7 +958,7 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
              P::SE_WORDS, P::SE_WORDS, v.raw);
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
-  launch_sa<N>(v, pk_in_sk, P::SK, n, st);
+  launch_sa<N, AES>(v, pk_in_sk, P::SK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
              v.sp8, v.ep16, v.epp16, v.part, v.seeds, (const uint8_t*)(v.seeds + 12), (size_t)128, nullptr, ct, sk,
              (size_t)P::SK, v.kk);
@@ -775,7 +966,7 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   return hipGetLastError();
 }
 
-template <int N>
+template <int N, bool AES>
 hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
   using P = FP<N>;
   const size_t C = round64(n);
@@ -787,8 +978,15 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   // S^T -> sp8 ([8][NP] int8), E -> ep16 as [N][8]
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
-  QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
-             v.sp8, v.ep16, v.part);
+  if constexpr (AES) {
+    QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
+               (size_t)P::PK, n, v.aesp);
+    QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * ((N + 255) / 256))), dim3(256), 0,
+               st, v.aesp, n, v.sp8, v.ep16, v.part);
+  } else {
+    QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
+               v.sp8, v.ep16, v.part);
+  }
   QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(256), 0, st, n, v.part, v.sp8, pk, sk);
   QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, n, sk);
   return hipGetLastError();
@@ -817,11 +1015,13 @@ size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk) {
 hipError_t frodo_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
                          const Streams& s) {
   if (n == 0) return hipSuccess;
-  if (a.aes) return hipErrorNotSupported;
-  switch (a.k) {
-    case 640: return frodo::keypair_t<640>(n, pk, sk, coins, scratch, s.main);
-    case 976: return frodo::keypair_t<976>(n, pk, sk, coins, scratch, s.main);
-    case 1344: return frodo::keypair_t<1344>(n, pk, sk, coins, scratch, s.main);
+  switch (a.k * 2 + (a.aes ? 1 : 0)) {
+    case 1280: return frodo::keypair_t<640, false>(n, pk, sk, coins, scratch, s.main);
+    case 1281: return frodo::keypair_t<640, true>(n, pk, sk, coins, scratch, s.main);
+    case 1952: return frodo::keypair_t<976, false>(n, pk, sk, coins, scratch, s.main);
+    case 1953: return frodo::keypair_t<976, true>(n, pk, sk, coins, scratch, s.main);
+    case 2688: return frodo::keypair_t<1344, false>(n, pk, sk, coins, scratch, s.main);
+    case 2689: return frodo::keypair_t<1344, true>(n, pk, sk, coins, scratch, s.main);
   }
   return hipErrorInvalidValue;
 }
@@ -829,11 +1029,13 @@ hipError_t frodo_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, c
 hipError_t frodo_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                         void* scratch, const Streams& s) {
   if (n == 0) return hipSuccess;
-  if (a.aes) return hipErrorNotSupported;
-  switch (a.k) {
-    case 640: return frodo::encaps_t<640>(n, ct, ss, pk, coins, scratch, s.main);
-    case 976: return frodo::encaps_t<976>(n, ct, ss, pk, coins, scratch, s.main);
-    case 1344: return frodo::encaps_t<1344>(n, ct, ss, pk, coins, scratch, s.main);
+  switch (a.k * 2 + (a.aes ? 1 : 0)) {
+    case 1280: return frodo::encaps_t<640, false>(n, ct, ss, pk, coins, scratch, s.main);
+    case 1281: return frodo::encaps_t<640, true>(n, ct, ss, pk, coins, scratch, s.main);
+    case 1952: return frodo::encaps_t<976, false>(n, ct, ss, pk, coins, scratch, s.main);
+    case 1953: return frodo::encaps_t<976, true>(n, ct, ss, pk, coins, scratch, s.main);
+    case 2688: return frodo::encaps_t<1344, false>(n, ct, ss, pk, coins, scratch, s.main);
+    case 2689: return frodo::encaps_t<1344, true>(n, ct, ss, pk, coins, scratch, s.main);
   }
   return hipErrorInvalidValue;
 }
@@ -841,11 +1043,13 @@ hipError_t frodo_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, co
 hipError_t frodo_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
                         const Streams& s) {
   if (n == 0) return hipSuccess;
-  if (a.aes) return hipErrorNotSupported;
-  switch (a.k) {
-    case 640: return frodo::decaps_t<640>(n, ss, ct, sk, scratch, s.main);
-    case 976: return frodo::decaps_t<976>(n, ss, ct, sk, scratch, s.main);
-    case 1344: return frodo::decaps_t<1344>(n, ss, ct, sk, scratch, s.main);
+  switch (a.k * 2 + (a.aes ? 1 : 0)) {
+    case 1280: return frodo::decaps_t<640, false>(n, ss, ct, sk, scratch, s.main);
+    case 1281: return frodo::decaps_t<640, true>(n, ss, ct, sk, scratch, s.main);
+    case 1952: return frodo::decaps_t<976, false>(n, ss, ct, sk, scratch, s.main);
+    case 1953: return frodo::decaps_t<976, true>(n, ss, ct, sk, scratch, s.main);
+    case 2688: return frodo::decaps_t<1344, false>(n, ss, ct, sk, scratch, s.main);
+    case 2689: return frodo::decaps_t<1344, true>(n, ss, ct, sk, scratch, s.main);
   }
   return hipErrorInvalidValue;
 }

@@ -1,4 +1,4 @@
-"""HIP FrodoKEM-SHAKE parity vs the oracle, through the C ABI (libqrkem.so).
+"""HIP FrodoKEM (SHAKE and AES Gen(A)) parity vs the oracle, through the C ABI (libqrkem.so).
 
 Bar: byte-exact pk / sk / ct / ss for every index (integer work).  The oracle
 (oracle/src/frodo.c, pinned to the Python restatement oracle/py/frodo_spec.py via
@@ -15,8 +15,10 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-ALGS = ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-1344-SHAKE"]
-SEC = {"FrodoKEM-640-SHAKE": 16, "FrodoKEM-976-SHAKE": 24, "FrodoKEM-1344-SHAKE": 32}
+ALGS = ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-1344-SHAKE",
+        "FrodoKEM-640-AES", "FrodoKEM-976-AES", "FrodoKEM-1344-AES"]
+SEC = {a: {"640": 16, "976": 24, "1344": 32}[a.split("-")[1]] for a in ALGS}
+GOLDEN_ALGS = ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-1344-SHAKE", "FrodoKEM-640-AES"]
 
 
 @pytest.fixture(scope="module")
@@ -65,7 +67,7 @@ def test_encaps_decaps_on_oracle_keys(engines, alg):
     """Encaps / Decaps alone (keys from the oracle), crossing the 256-handshake sub-chunk."""
     import oracle as orc
     eng = engines[alg]
-    n = 300 if alg == "FrodoKEM-640-SHAKE" else 97
+    n = 300 if alg.startswith("FrodoKEM-640") else 97
     kc, ec = _coins(alg, n, 8)
     opk, osk = orc.batch_keypair(alg, kc, 8)
     oct_, oss = orc.batch_encaps(alg, opk, ec, 8)
@@ -100,7 +102,7 @@ def test_tampered_implicit_rejection(engines, alg):
     assert not np.any(np.all(ss[flip] == oss[flip], axis=1))
 
 
-@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("alg", GOLDEN_ALGS)
 def test_kat_drbg_records_match_golden(engines, golden_dir, alg):
     """NIST-KAT-DRBG coins, digests of the Python restatement (tests/golden/kat_frodo.json)."""
     import oracle as orc
@@ -117,12 +119,13 @@ def test_kat_drbg_records_match_golden(engines, golden_dir, alg):
         assert hashlib.sha256(arr.tobytes()).hexdigest() == g["digests"][name], name
 
 
-def test_multichunk_640(engines):
+@pytest.mark.parametrize("alg", ["FrodoKEM-640-SHAKE", "FrodoKEM-640-AES"])
+def test_multichunk_640(engines, alg):
     """More handshakes than one Frodo chunk (2^14 cap lowered via set_chunk): ss_enc == ss_dec
     everywhere, a sample byte-exact vs the oracle."""
     import oracle as orc
     from qrkem.batch import BatchKEM
-    alg, n = "FrodoKEM-640-SHAKE", 1200
+    n = 1200
     eng = BatchKEM(alg, device=0, chunk=512)
     coins = eng.bench_coins(n, 64, seed=42)
     kc, ec = coins[:, :48].contiguous(), coins[:, 48:].contiguous()
