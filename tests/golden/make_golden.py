@@ -12,7 +12,8 @@ Fixtures:
                   plus the first records in full.  1024 records for ML-KEM-768
                   (BASELINE.json configs[0]), 100 for ML-KEM-512/1024.
   kat_frodo.json  the same procedure for FrodoKEM-640/976/1344-SHAKE (10 records)
-                  and FrodoKEM-640-AES (1 record; pure-Python AES is slow).
+                  and FrodoKEM-640/976/1344-AES (1 record each; pure-Python AES is slow;
+                  976/1344-AES were appended with kat_records(F, alg, 1, ...) directly).
   tampered.json   ML-KEM-768 decapsulation of bit-flipped ciphertexts
                   (implicit rejection K_bar = J(z || c')).
   coins.json      bench coin derivation SHAKE256("qrk-bench"||LE64 seed||LE64 i).

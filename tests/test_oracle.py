@@ -74,7 +74,7 @@ def test_c_oracle_matches_golden_mlkem(golden_dir, alg):
 
 
 @pytest.mark.parametrize("alg", ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-1344-SHAKE",
-                                 "FrodoKEM-640-AES"])
+                                 "FrodoKEM-640-AES", "FrodoKEM-976-AES", "FrodoKEM-1344-AES"])
 def test_c_oracle_matches_golden_frodo(golden_dir, alg):
     _kat_check(json.loads((golden_dir / "kat_frodo.json").read_text()), alg)
 
