@@ -140,6 +140,9 @@ def kernel_ops_per_hs(alg, name, mode):
     return None, None
 
 
+RED_DEVICE = None  # device of the end-of-run reduction tensors (None = host, for gloo)
+
+
 # ---------------------------------------------------------------- helpers
 def env_int(name, default):
     v = os.environ.get(name)
@@ -350,7 +353,7 @@ def bench_handshake(args, world, rank, local):
     prof = e.profile_read() if not args.no_profile else {}
     e.profile(False)
     disagree = int((out.agree != 1).sum().item())
-    elapsed, (disagree,) = reduce_run(elapsed, [disagree], device=f"cuda:{local}")
+    elapsed, (disagree,) = reduce_run(elapsed, [disagree], device=RED_DEVICE)
     value = B * world * args.steps / elapsed
     W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric])
     k = KP[alg][0]
@@ -427,9 +430,21 @@ def main():
     local = env_int("LOCAL_RANK", 0)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # One rank per GPU over RCCL ("nccl").  QRK_BENCH_BACKEND=gloo with more ranks than GPUs
+    # rehearses the multi-rank path on a single card (never used for scaling numbers).
+    global RED_DEVICE
+    backend = os.environ.get("QRK_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} GPUs visible")
+    local %= max(ndev, 1)
     torch.cuda.set_device(local)
+    RED_DEVICE = f"cuda:{local}" if backend == "nccl" else None
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     if args.mode == "handshake":
         return bench_handshake(args, world, rank, local)
@@ -523,7 +538,7 @@ def main():
         # valid rows must give the encapsulated key, tampered rows the implicit-rejection key
         bad = int((same != ~tampered).sum().item())
         counters = [bad, int(tampered.sum().item())]
-    elapsed, (bad, n_tampered) = reduce_run(elapsed, counters, device=f"cuda:{local}")
+    elapsed, (bad, n_tampered) = reduce_run(elapsed, counters, device=RED_DEVICE)
     if args.mode == "encdec":
         checks["ss_enc_eq_ss_dec_mismatches"] = bad
     else:
