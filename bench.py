@@ -410,6 +410,127 @@ def bench_handshake(args, world, rank, local):
         dist.destroy_process_group()
 
 
+# ---------------------------------------------------------------- wire mode
+HBM_PEAK = 8.0e12  # B/s, MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def bench_wire(args, world, rank, local):
+    """One step = the base64 work of B key exchanges: encode pk_i (messaging.py:607), decode it
+    (:829), encode ct and pk_r (:852-853), decode ct (:1037).  value = handshakes/s."""
+    from qrkem.shard import reduce_run
+    from qrkem.wire import Base64Codec, encoded_len
+    alg = args.alg
+    if alg not in KP:
+        raise SystemExit("wire mode: ML-KEM algorithms only in the bench")
+    lb = args.log2_batch if args.log2_batch is not None else 20
+    B = 1 << lb
+    PK, _, CT = mlkem_sizes(alg)
+    codec = Base64Codec(device=local)
+    g = torch.Generator(device=f"cuda:{local}").manual_seed(args.seed + rank)
+    pk_i = torch.randint(0, 256, (B, PK), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
+    pk_r = torch.randint(0, 256, (B, PK), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
+    ct_ = torch.randint(0, 256, (B, CT), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
+
+    def step():
+        t_pk = codec.encode(pk_i)
+        pk_rx, st1 = codec.decode(t_pk, PK)
+        t_ct = codec.encode(ct_)
+        t_pkr = codec.encode(pk_r)
+        ct_rx, st2 = codec.decode(t_ct, CT)
+        return t_pk, t_ct, t_pkr, pk_rx, ct_rx, st1, st2
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        _ctx_profile(codec, True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = _ctx_profile_read(codec) if not args.no_profile else {}
+    t_pk, t_ct, t_pkr, pk_rx, ct_rx, st1, st2 = out
+    bad = int((pk_rx != pk_i).any(dim=1).sum().item() + (ct_rx != ct_).any(dim=1).sum().item()
+              + st1.abs().sum().item() + st2.abs().sum().item())
+    elapsed, (bad,) = reduce_run(elapsed, [bad], device=RED_DEVICE)
+    value = B * world * args.steps / elapsed
+    epk, ect = encoded_len(PK), encoded_len(CT)
+    bytes_hs = 2 * (PK + epk) + (epk + PK + 4) + (CT + ect) + (ect + CT + 4)
+    kernels, roof = {}, None
+    per = {"k_b64_encode": 2 * (PK + epk) + (CT + ect), "k_b64_decode": (epk + PK + 4) + (ect + CT + 4)}
+    for name, (ms, cnt) in prof.items():
+        kernels[name] = {"avg_ms": ms / cnt, "launches": cnt}
+        if name in per:
+            rate = per[name] * B * args.steps / (ms * 1e-3)
+            kernels[name].update(bound="hbm", achieved_GBs=rate / 1e9, frac=rate / HBM_PEAK)
+    if prof:
+        dom = max((k for k in prof if k in per), key=lambda k: prof[k][0])
+        ms, cnt = prof[dom]
+        rate = per[dom] * B * args.steps / (ms * 1e-3)
+        roof = {"kernel": dom, "bound": "hbm", "achieved": rate / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": rate / HBM_PEAK, "traffic": None, "avg_launch_ms": ms / cnt,
+                "algorithmic_bytes_per_launch": per[dom] * B * args.steps / cnt}
+    result = {
+        "metric": f"{alg} wire-field base64 codec, handshakes/sec at batch 2^{lb} per GPU "
+                  f"(encode pk_i, pk_r, ct; decode pk_i, ct)",
+        "value": value, "unit": "handshakes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: uniformly random pk / ct bytes of the ML-KEM sizes, device-resident",
+        "config": {"workload": f"{alg} KEM wire fields of 2^{lb} exchanges per GPU (SURVEY.md 8f-3)",
+                   "alg": alg, "batch_per_gpu": B, "global_batch": B * world, "bytes_per_handshake": bytes_hs,
+                   "parallelism": f"index-sharded x{world} (no data-path collective)"},
+        "roofline": roof, "hbm_GBs_step": value * bytes_hs / 1e9, "kernels_timed_region": kernels,
+        "checks": {"roundtrip_mismatches_or_rejects": bad}, "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import base64
+        S = 1 << 14
+        h_pk, h_pkr, h_ct = (np.ascontiguousarray(t[:S].cpu().numpy()) for t in (pk_i, pk_r, ct_))
+        t0 = time.perf_counter()
+        m = 0
+        while time.perf_counter() - t0 < 10.0 and m < S:  # the reference call pattern, one field per call
+            a = base64.b64encode(h_pk[m].tobytes()).decode()
+            base64.b64decode(a)
+            c = base64.b64encode(h_ct[m].tobytes()).decode()
+            base64.b64encode(h_pkr[m].tobytes()).decode()
+            base64.b64decode(c)
+            m += 1
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": m / dt, "unit": "handshakes/s", "cores": 1, "kind": "reference",
+                                  "sample": f"{m} handshakes' fields through Python base64 (the reference's own "
+                                            f"calls, messaging.py:607, 829, 852-853, 1037), one core"}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _ctx_profile(obj, on):
+    from qrkem._native import LIB
+    LIB.qrk_ctx_profile(obj._ctx, int(on))
+
+
+def _ctx_profile_read(obj):
+    import ctypes as ct
+    from qrkem._native import LIB
+    n = LIB.qrk_ctx_profile_collect(obj._ctx)
+    out = {}
+    for i in range(max(n, 0)):
+        name, ms, cnt = ct.c_char_p(), ct.c_double(), ct.c_uint64()
+        LIB.qrk_ctx_profile_get(obj._ctx, i, ct.byref(name), ct.byref(ms), ct.byref(cnt))
+        out[name.value.decode()] = (ms.value, cnt.value)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -419,7 +540,7 @@ def main():
     ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM)")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
-    ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake"], default="encdec")
+    ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -448,6 +569,8 @@ def main():
 
     if args.mode == "handshake":
         return bench_handshake(args, world, rank, local)
+    if args.mode == "wire":
+        return bench_wire(args, world, rank, local)
     from qrkem.batch import BatchKEM
     from qrkem.shard import reduce_run, weak_shard
     alg = args.alg

@@ -175,6 +175,18 @@ int qrk_handshake_batch(qrk_ctx *ctx, const char *alg, size_t n, const uint8_t *
                         const uint64_t *info_off, size_t info_len, size_t key_len, uint8_t *pk_i, uint8_t *pk_r,
                         uint8_t *ct, uint8_t *key_i, uint8_t *key_r, int32_t *agree, void *stream);
 
+/* Wire format: standard base64 (RFC 4648 section 4, '=' padding), the encoding the reference
+ * puts every KEM payload in before JSON framing (messaging.py:607 public key, :852-853
+ * ciphertext and responder key; decoded at :829 with base64.b64decode).  Device pointers,
+ * contiguous records.  Encode: in [n][in_len] -> out [n][4*ceil(in_len/3)] ASCII (no NUL).
+ * Decode (strict): in [n][4*ceil(out_len/3)] -> out [n][out_len]; status (nullable, int32[n])
+ * = -1 for a record with a byte outside the alphabet or misplaced / missing padding, else 0.
+ * (Python's b64decode without validate=True would silently skip such bytes; a malformed KEM
+ * field is rejected here instead.) */
+int qrk_base64_encode_batch(qrk_ctx *ctx, size_t n, const uint8_t *in, size_t in_len, uint8_t *out, void *stream);
+int qrk_base64_decode_batch(qrk_ctx *ctx, size_t n, const uint8_t *in, size_t out_len, uint8_t *out,
+                            int32_t *status, void *stream);
+
 /* Per-kernel HIP-event timing on the launch stream (for bench.py's roofline).
  * qrk_ctx_profile(ctx, 1) resets and enables; qrk_ctx_profile_collect()
  * synchronises the recorded events and returns the number of distinct kernel

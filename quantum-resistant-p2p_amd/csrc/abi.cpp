@@ -684,6 +684,29 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
   return e == hipSuccess ? 0 : hip_fail("hipMemsetAsync(cleanse)", e);
 }
 
+int qrk_base64_encode_batch(qrk_ctx* ctx, size_t n, const uint8_t* in, size_t in_len, uint8_t* out, void* stream) {
+  if (!ctx) return fail("null context");
+  if (n && in_len && (!in || !out)) return fail("null buffer");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (ensure_device(ctx->device)) return -1;
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  hipError_t e = base64_encode(n, in, in_len, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("base64_encode", e);
+}
+
+int qrk_base64_decode_batch(qrk_ctx* ctx, size_t n, const uint8_t* in, size_t out_len, uint8_t* out, int32_t* status,
+                            void* stream) {
+  if (!ctx) return fail("null context");
+  if (n && out_len && (!in || !out)) return fail("null buffer");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (ensure_device(ctx->device)) return -1;
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  hipError_t e = hipSuccess;
+  if (status && n) e = hipMemsetAsync(status, 0, n * sizeof(int32_t), (hipStream_t)stream);
+  if (e == hipSuccess) e = base64_decode(n, in, out_len, out, status, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("base64_decode", e);
+}
+
 const char* qrk_last_error(void) { return g_err.c_str(); }
 
 int qrk_device_count(void) {

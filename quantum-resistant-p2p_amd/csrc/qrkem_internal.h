@@ -90,4 +90,9 @@ hipError_t hkdf_sha256(size_t n, const uint8_t* ikm, size_t ikm_len, size_t ikm_
 // agree_i = (a_i == b_i), len bytes each
 hipError_t keys_equal(size_t n, const uint8_t* a, const uint8_t* b, size_t len, int32_t* agree, hipStream_t st);
 
+// Standard base64 (RFC 4648, '=' padding) of n records of L bytes -> [n][4 ceil(L/3)] chars,
+// and strict decoding back (status[i] = -1 for a malformed record; caller zeroes status).
+hipError_t base64_encode(size_t n, const uint8_t* in, size_t L, uint8_t* out, hipStream_t st);
+hipError_t base64_decode(size_t n, const uint8_t* in, size_t L, uint8_t* out, int32_t* status, hipStream_t st);
+
 }  // namespace qrk

@@ -55,6 +55,8 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_tamper": (ct.c_int, [P, SZ, SZ, ct.c_uint64, ct.c_int, P, P]),
         "qrk_hkdf_sha256_batch": (ct.c_int, [P, SZ, P, SZ, P, SZ, P, P, SZ, P, SZ, P]),
         "qrk_handshake_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P, P, SZ, SZ, P, P, P, P, P, P, P]),
+        "qrk_base64_encode_batch": (ct.c_int, [P, SZ, P, SZ, P, P]),
+        "qrk_base64_decode_batch": (ct.c_int, [P, SZ, P, SZ, P, P, P]),
         "qrk_ctx_profile": (ct.c_int, [P, ct.c_int]),
         "qrk_ctx_profile_collect": (ct.c_int, [P]),
         "qrk_ctx_profile_get": (ct.c_int, [P, ct.c_int, ct.POINTER(ct.c_char_p), ct.POINTER(ct.c_double),

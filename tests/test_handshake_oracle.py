@@ -95,3 +95,17 @@ def test_handshake_driver_vs_single_calls():
         assert ct_ == c[i].tobytes()
         assert hkdf_spec.hkdf_sha256(ss, infos[i], 32) == key_r[i].tobytes()
         assert orc.keypair(alg, kpr[i].tobytes())[0] == pk_r[i].tobytes()
+
+
+def test_wire_oracle_is_python_base64():
+    import base64
+    import wire_spec
+    rng = np.random.default_rng(9)
+    d = rng.integers(0, 256, (4, 1184), dtype=np.uint8)
+    enc = wire_spec.encode_records(d)
+    assert enc.shape == (4, 1580)
+    for i in range(4):
+        assert enc[i].tobytes() == base64.b64encode(d[i].tobytes())
+        assert wire_spec.decode_record(enc[i].tobytes(), 1184) == d[i].tobytes()
+    assert wire_spec.decode_record(b"QUJD!A==", 4) is None
+    assert wire_spec.decode_record(b"QUJD", 2) is None
