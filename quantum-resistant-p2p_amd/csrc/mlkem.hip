@@ -187,6 +187,16 @@ __device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, i
 // the consumer reads them without any parsing.  inst = (x*K + y) * C + hs.
 constexpr int MAX_XOF_BLOCKS = 16;
 
+// Occupancy hints (waves per SIMD lower bound; tuning knobs)
+#ifndef QRK_WPE_CORE
+#define QRK_WPE_CORE 1
+#endif
+#ifndef QRK_WPE_FRONT
+#define QRK_WPE_FRONT 1
+#endif
+#define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
+#define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
+
 // Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
 // flushing completed 8-coefficient chunks to dst.
 __device__ __forceinline__ void compact_block(const KState& s, uint32_t* ring, int& cnt, uint4* dst) {
@@ -349,7 +359,7 @@ __global__ __launch_bounds__(256) void k_back_keygen(const uint8_t* __restrict__
 
 // Encaps front: (K, r) = G(m || H(ek)); K -> ss, r -> seeds
 template <int K>
-__global__ __launch_bounds__(256) void k_front_encaps(const uint8_t* __restrict__ pk,
+__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_encaps(const uint8_t* __restrict__ pk,
                                                       const uint8_t* __restrict__ coins, size_t n,
                                                       uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
   const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -374,7 +384,7 @@ __global__ __launch_bounds__(256) void k_front_encaps(const uint8_t* __restrict_
 
 // Decaps front: (K', r') = G(m' || h), Kbar = J(z || c)
 template <int K>
-__global__ __launch_bounds__(256) void k_front_decaps(const uint8_t* __restrict__ ct,
+__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk,
                                                       const uint64_t* __restrict__ mprime, size_t n,
                                                       uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
@@ -409,11 +419,17 @@ struct P16 {
 // the stride image [L + 16m] and the contiguous image [16L + t] are conflict-free)
 // plus 84 words of byte staging (raw XOF blocks, bit-packed encodings).
 constexpr int PBUF = 272;
-constexpr int RAWW = 84;
+// 44 words of byte staging hold the largest packed polynomial (du = 11: 352 bytes).  The
+// group stride is 368 dwords = 16 (mod 32): the two 16-lane groups that share a ds_* bank
+// half (lanes 0-31 / 32-63) then use disjoint bank sets for every access pattern above.
+constexpr int RAWW = 44;
+constexpr int GPAD = 8;
 struct GroupLds {
   int poly[PBUF];
   uint64_t raw[RAWW];
+  int pad[GPAD];
 };
+static_assert(sizeof(GroupLds) / 4 % 32 == 16, "group stride must be 16 mod 32 dwords");
 constexpr int GROUPS = 16;  // 256 threads
 
 __device__ __forceinline__ void stride_to_contig(P16& p, int* buf, int L) {
@@ -993,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
 template <int K, int MODE>
-__global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
@@ -1103,7 +1119,7 @@ __global__ __launch_bounds__(256) void k_encrypt_core(size_t n, size_t C, const 
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K>
-__global__ __launch_bounds__(256) void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
+__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   __shared__ GroupLds lds[GROUPS];

@@ -9,7 +9,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 C=$R/quantum-resistant-p2p_amd/csrc
 O=$R/build/variant_$tag
 mkdir -p "$O" "$R/quantum-resistant-p2p_amd/qrkem/variants"
-for f in mlkem util frodo hkdf; do
+for f in $(cd "$C" && ls *.hip | sed "s/\.hip$//"); do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c "$C/$f.hip" -o "$O/$f.o" &
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -fPIC -std=c++17 "$@" -c "$C/abi.cpp" -o "$O/abi.o" &
