@@ -197,9 +197,26 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
 #define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
 
+// (a & m) | b as one v_and_or_b32 (LLVM rewrites a disjoint OR into and + add)
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(b));
+  return r;
+}
+// (a << s) | b as one v_lshl_or_b32
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
+  return r;
+}
+
 // Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
 // flushing completed 8-coefficient chunks to dst.
-__device__ __forceinline__ void compact_block(const KState& s, uint32_t* ring, int& cnt, uint4* dst) {
+// `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
+// 8-11 are zero, so an entry address is one v_and_or_b32, (pos & 0xF00) | rb, with the static
+// LDS base folded into the ds_write offset.
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
+  const uint32_t* ring = (const uint32_t*)(ring_all + rb);
 #pragma unroll
   for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
     uint32_t d[3];
@@ -216,7 +233,7 @@ __device__ __forceinline__ void compact_block(const KState& s, uint32_t* ring, i
     int pos = cnt << 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      *(uint32_t*)((char*)ring + (pos & 0xF00)) = (uint32_t)c[e];
+      *(uint32_t*)(ring_all + and_or(pos, 0xF00u, rb)) = (uint32_t)c[e];
       pos += c[e] < Q ? 256 : 0;
     }
     cnt = pos >> 8;
@@ -225,7 +242,7 @@ __device__ __forceinline__ void compact_block(const KState& s, uint32_t* ring, i
       const uint32_t* r = ring + (ch & 1) * 8 * 64;
       uint32_t w[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = r[(2 * j) * 64] | (r[(2 * j + 1) * 64] << 16);
+      for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 64], 16, r[(2 * j) * 64]);
       dst[ch * 64] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
@@ -241,7 +258,7 @@ __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_bas
                                              size_t n, size_t C, uint4* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
-  uint32_t* ring = ring_all + (threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63);
+  const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;
   const size_t stride = FIX ? (size_t)gridDim.x * 256 : 0;
   size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t limit = FIX ? (size_t)*nfix : (size_t)K * K * C;
@@ -263,7 +280,7 @@ __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_bas
 #pragma unroll 1
     for (int b = 0; b < (FIX ? MAX_XOF_BLOCKS : 3) && (!FIX || cnt < 256); ++b) {
       keccak_f(s);
-      compact_block(s, ring, cnt, dst);
+      compact_block(s, (char*)ring_all, rb, cnt, dst);
     }
     if (!FIX) {
       if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
@@ -876,6 +893,33 @@ __device__ __forceinline__ void flush_bits(GroupLds& g, uint8_t* dst, const uint
   gsync();
 }
 
+// Decaps compare with the received ciphertext words loaded ahead of time (cmp_load):
+// the global-load latency hides behind the row's NTT work instead of stalling the flush.
+template <int D>
+struct CmpWords {
+  uint32_t w[(8 * D + 15) / 16];
+};
+template <int D>
+__device__ __forceinline__ CmpWords<D> cmp_load(const uint8_t* cmp, int L) {
+  CmpWords<D> r;
+#pragma unroll
+  for (int i = 0; i < (8 * D + 15) / 16; ++i) {
+    const int idx = L + 16 * i;
+    r.w[i] = idx < 8 * D ? ((const uint32_t*)cmp)[idx] : 0u;
+  }
+  return r;
+}
+template <int D>
+__device__ __forceinline__ void flush_cmp(GroupLds& g, const CmpWords<D>& c, uint32_t& diff, int L) {
+  const uint32_t* st = (const uint32_t*)g.raw;
+#pragma unroll
+  for (int i = 0; i < (8 * D + 15) / 16; ++i) {
+    const int idx = L + 16 * i;
+    if (idx < 8 * D) diff |= st[idx] ^ c.w[i];
+  }
+  gsync();
+}
+
 // SampleNTT consumer: lane L loads coefficients 16L..16L+15 (chunks 2L, 2L+1)
 // of the producer's compacted output -- contiguous layout, no parsing.
 __device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t inst, int L) {
@@ -970,29 +1014,43 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   BOp sb[K];
+  {
+    CbdRaw sr[K];  // every s_j's CBD words issued before the first NTT
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    PF16 f;
-    cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L));
-    contig_to_stride_f(f, (float*)g.poly, L);
-    ntt_fwd_f<false>(f, (float*)g.poly, L);
-    sb[j] = make_bop_f(f, L);
-    P16 t;
+    for (int j = 0; j < K; ++j) sr[j] = cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L);
 #pragma unroll
-    for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
-    if (active) encode12(t, dk + 384 * j, L);
+    for (int j = 0; j < K; ++j) {
+      PF16 f;
+      cbd_f<P<K>::ETA1>(f, sr[j]);
+      contig_to_stride_f(f, (float*)g.poly, L);
+      ntt_fwd_f<false>(f, (float*)g.poly, L);
+      sb[j] = make_bop_f(f, L);
+      P16 t;
+#pragma unroll
+      for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
+      if (active) encode12(t, dk + 384 * j, L);
+    }
   }
+  // row i's matrix entries and e_i's CBD words are loaded one row ahead
+  PK8 an[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)(j * K) * C + hs, L);
+  CbdRaw er = cbd_load<P<K>::ETA1>(prf, (size_t)K * C + hs, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(j * K + i) * C + hs, L), sb[j]);
+    for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], sb[j]);
+    const CbdRaw ecur = er;
+    if (i + 1 < K) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)(j * K + i + 1) * C + hs, L);
+      er = cbd_load<P<K>::ETA1>(prf, (size_t)(K + i + 1) * C + hs, L);
     }
     PF16 ef;
-    cbd_f<P<K>::ETA1>(ef, cbd_load<P<K>::ETA1>(prf, (size_t)(K + i) * C + hs, L));
+    cbd_f<P<K>::ETA1>(ef, ecur);
     contig_to_stride_f(ef, (float*)g.poly, L);
     ntt_fwd_f<false>(ef, (float*)g.poly, L);
     P16 t;
@@ -1064,6 +1122,8 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
 #pragma unroll
     for (int t = 0; t < 16; ++t) uf.v[t] = acc_to_f(acc[t]);
     ntt_inv_f(uf, (float*)g.poly, L);
+    CmpWords<DU> cw;
+    if (MODE) cw = cmp_load<DU>(c + 32 * DU * i, L);
     stride_to_contig_f(uf, (float*)g.poly, L);
     PF16 ef;
     cbd_f<P<K>::ETA2>(ef, ecur);
@@ -1071,7 +1131,10 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
 #pragma unroll
     for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon_f(uf.v[t] + ef.v[t]));
     pack_bits<DU>(u, g, L);
-    flush_bits<DU>(g, c + 32 * DU * i, MODE ? c + 32 * DU * i : nullptr, diff, active, L);
+    if (MODE)
+      flush_cmp<DU>(g, cw, diff, L);
+    else
+      flush_bits<DU>(g, c + 32 * DU * i, nullptr, diff, active, L);
   }
   // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
   {

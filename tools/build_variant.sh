@@ -1,12 +1,12 @@
 #!/bin/bash
 # Build an experimental libqrkem variant with extra -D flags (kernel tuning sweeps):
-#   tools/build_variant.sh <tag> -DQRK_AES_COLS=16 ...
+#   [CSRC=<other csrc dir>] tools/build_variant.sh <tag> -DQRK_AES_COLS=16 ...
 # Output: quantum-resistant-p2p_amd/qrkem/variants/libqrkem_<tag>.so (git-ignored; load it
 # with QRKEM_LIBRARY=<path>).  The default build is untouched.
 set -euo pipefail
 tag=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
-C=$R/quantum-resistant-p2p_amd/csrc
+C=${CSRC:-$R/quantum-resistant-p2p_amd/csrc}
 O=$R/build/variant_$tag
 mkdir -p "$O" "$R/quantum-resistant-p2p_amd/qrkem/variants"
 for f in $(cd "$C" && ls *.hip | sed "s/\.hip$//"); do
