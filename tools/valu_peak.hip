@@ -119,6 +119,12 @@ MKK(sub_sdwa, "v_sub_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src
 MKK(bfe_i32, "v_bfe_i32 %0, %0, 0, 16 ; %1", seed)
 MKK(med3_i32, "v_med3_i32 %0, %0, %1, %1", seed)
 MKK(cndmask, "v_cndmask_b32 %0, %0, %1, vcc", seed)
+MKK(cndmask_e64, "v_cndmask_b32_e64 %0, %0, %1, s[4:5]", seed)
+MKK(cmp_cndmask, "v_cmp_gt_u32 vcc, %1, %0\n v_cndmask_b32 %0, %0, %1, vcc", seed)
+MKK(cmp_addc, "v_cmp_gt_u32 vcc, %1, %0\n v_addc_co_u32 %0, vcc, 0, %0, vcc", seed)
+MKK(sub_ashr, "v_sub_u32 %0, %0, %1\n v_ashrrev_i32 %0, 1, %0", seed)
+MKK(and_or, "v_and_or_b32 %0, %0, %1, %1", seed)
+MKK(lshl_or, "v_lshl_or_b32 %0, %0, 3, %1", seed)
 
 // 64-bit register (packed fp32) ops: instruction rate (each instruction = 2 fp32 lanes)
 #define MKK64(NAME, INSTR, INIT_B)                                                            \
@@ -175,6 +181,8 @@ int main() {
             {"cvt_i32_f32", k_cvt_i32_f32}, {"mad_i32_i16", k_mad_i32_i16}, {"mad_u32_u16", k_mad_u32_u16},
             {"mul_hi_i32", k_mul_hi_i32}, {"pk_mad_i16", k_pk_mad_i16}, {"sub_sdwa", k_sub_sdwa},
             {"bfe_i32", k_bfe_i32}, {"med3_i32", k_med3_i32}, {"cndmask", k_cndmask},
+            {"cndmask_e64", k_cndmask_e64}, {"cmp_cndmask_pair", k_cmp_cndmask}, {"cmp_addc_pair", k_cmp_addc},
+            {"sub_ashr_pair", k_sub_ashr}, {"and_or", k_and_or}, {"lshl_or", k_lshl_or},
             {"pk_fma_f32_instr", k_pk_fma_f32}, {"pk_mul_f32_instr", k_pk_mul_f32}, {"pk_add_f32_instr", k_pk_add_f32}};
   for (auto& k : ks) {
     hipLaunchKernelGGL(k.fn, dim3(blocks), dim3(threads), 0, 0, d, 1u);
