@@ -127,6 +127,11 @@ struct qrk_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* hs_scratch = nullptr;  // handshake driver: ephemeral sk / ss of one chunk
   size_t hs_scratch_bytes = 0;
+  uint8_t* dio = nullptr;         // host-pointer calls: packed device inputs | outputs
+  size_t dio_bytes = 0;
+  uint8_t* hio = nullptr;         // ... and their pinned host mirror
+  size_t hio_bytes = 0;
+  hipStream_t io_stream = nullptr;
   int streams = 2;            // 1: serial schedule (kernel timings in isolation), 2: forked
   std::mutex mu;
 };
@@ -245,6 +250,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   }
   Streams S;
   S.main = st;
+  // (the fork also shortens single-shot latency: the SampleNTT chain runs beside front + PRF)
   S.aux = ctx->streams > 1 ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
@@ -291,7 +297,10 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   return 0;
 }
 
-// Host-pointer wrapper: stage inputs, run, copy outputs back, synchronise.
+// Host-pointer wrapper: stage inputs, run, copy outputs back, synchronise.  The context
+// keeps a device I/O buffer, a pinned host mirror and its own stream, so a call is one
+// packed H2D copy, the kernels, one packed D2H copy and one synchronise (the reference's
+// one-handshake-per-call pattern, oqs.py:318, 348, 372, pays no allocation per call).
 static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2,
                           const uint8_t* i1, const uint8_t* i2, int32_t* status) {
   if (n == 0) return 0;
@@ -304,31 +313,34 @@ static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   }
   const size_t l_st = status ? sizeof(int32_t) : 0;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  const size_t b_o1 = al(n * l_o1), b_o2 = al(n * l_o2), b_i1 = al(n * l_i1), b_i2 = al(n * l_i2),
+  // inputs first (one H2D), then outputs (one D2H)
+  const size_t b_i1 = al(n * l_i1), b_i2 = al(n * l_i2), b_o1 = al(n * l_o1), b_o2 = al(n * l_o2),
                b_st = al(n * l_st);
-  uint8_t* d = nullptr;
-  hipError_t e = hipMalloc((void**)&d, b_o1 + b_o2 + b_i1 + b_i2 + b_st + 256);
-  if (e != hipSuccess) return hip_fail("hipMalloc(stage)", e);
-  uint8_t *d_o1 = d, *d_o2 = d_o1 + b_o1, *d_i1 = d_o2 + b_o2, *d_i2 = d_i1 + b_i1, *d_st = d_i2 + b_i2;
-  hipStream_t st = nullptr;
-  int rc = 0;
-  if (l_i1) e = hipMemcpy(d_i1, i1, n * l_i1, hipMemcpyHostToDevice);
-  if (e == hipSuccess && l_i2) e = hipMemcpy(d_i2, i2, n * l_i2, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    rc = hip_fail("hipMemcpy(H2D)", e);
-  } else {
-    rc = run_batch(ctx, a, op, n, d_o1, l_o2 ? d_o2 : nullptr, l_i1 ? d_i1 : nullptr, l_i2 ? d_i2 : nullptr,
-                   status ? (int32_t*)d_st : nullptr, st);
-    if (!rc) {
-      e = hipStreamSynchronize(st);
-      if (e == hipSuccess) e = hipMemcpy(o1, d_o1, n * l_o1, hipMemcpyDeviceToHost);
-      if (e == hipSuccess && l_o2) e = hipMemcpy(o2, d_o2, n * l_o2, hipMemcpyDeviceToHost);
-      if (e == hipSuccess && status) e = hipMemcpy(status, d_st, n * l_st, hipMemcpyDeviceToHost);
-      if (e != hipSuccess) rc = hip_fail("kernel execution / D2H", e);
-    }
+  const size_t in_bytes = b_i1 + b_i2, out_bytes = b_o1 + b_o2 + b_st;
+  if (!ctx->io_stream) {
+    hipError_t e = hipStreamCreateWithFlags(&ctx->io_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail("hipStreamCreate(io)", e);
   }
-  (void)hipFree(d);
-  return rc;
+  hipStream_t st = ctx->io_stream;
+  if (grow_device((void**)&ctx->dio, &ctx->dio_bytes, in_bytes + out_bytes, st)) return -1;
+  if (grow_pinned(&ctx->hio, &ctx->hio_bytes, in_bytes + out_bytes)) return -1;
+  uint8_t *d_i1 = ctx->dio, *d_i2 = d_i1 + b_i1, *d_o1 = d_i2 + b_i2, *d_o2 = d_o1 + b_o1, *d_st = d_o2 + b_o2;
+  uint8_t* h = ctx->hio;
+  if (l_i1) memcpy(h, i1, n * l_i1);
+  if (l_i2) memcpy(h + b_i1, i2, n * l_i2);
+  hipError_t e = in_bytes ? hipMemcpyAsync(ctx->dio, h, in_bytes, hipMemcpyHostToDevice, st) : hipSuccess;
+  if (e != hipSuccess) return hip_fail("hipMemcpyAsync(H2D)", e);
+  int rc = run_batch(ctx, a, op, n, d_o1, l_o2 ? d_o2 : nullptr, l_i1 ? d_i1 : nullptr, l_i2 ? d_i2 : nullptr,
+                     status ? (int32_t*)d_st : nullptr, st);
+  if (rc) return rc;
+  uint8_t* ho = h + in_bytes;
+  e = hipMemcpyAsync(ho, d_o1, out_bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return hip_fail("kernel execution / D2H", e);
+  memcpy(o1, ho, n * l_o1);
+  if (l_o2) memcpy(o2, ho + b_o1, n * l_o2);
+  if (status) memcpy(status, ho + b_o1 + b_o2, n * l_st);
+  return 0;
 }
 
 // ------------------------------------------------------------------ default context (single-shot API)
@@ -488,12 +500,15 @@ int qrk_ctx_create(qrk_ctx** out, int device) {
 
 void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->scratch || ctx->dstage || ctx->aux) {
+  if (ctx->scratch || ctx->dstage || ctx->aux || ctx->dio) {
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
   }
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->hs_scratch) (void)hipFree(ctx->hs_scratch);
+  if (ctx->dio) (void)hipFree(ctx->dio);
+  if (ctx->hio) (void)hipHostFree(ctx->hio);
+  if (ctx->io_stream) (void)hipStreamDestroy(ctx->io_stream);
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
