@@ -211,6 +211,17 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
     }
 
 
+def keccak_practical_peak():
+    """Top/s (4320-op count) of a register-resident Keccak-f[1600] loop measured on MI355X by
+    tools/valu_peak.hip (profiles/r1/valu_peak_r1b.json), or None."""
+    f = ROOT / "profiles" / "r1" / "valu_peak_r1b.json"
+    try:
+        d = json.loads(f.read_text())
+        return max(v for k, v in d.items() if k.startswith("keccak_") and k.endswith("_Tops_at_4320"))
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(alg, mode, chunk, kernel):
     """HBM bytes per dispatch of `kernel` from the committed rocprofv3 PMC pass of the same
     configuration (profiles/pmc_traffic.json, written by tools/prof_summary.py), or None."""
@@ -687,6 +698,13 @@ def main():
         roof["traffic_source"] = src
         roof["algorithmic_ops_per_launch"] = roof.pop("ops_per_launch")
         roof["isolated_frac"] = roof_iso["frac"] if roof_iso and roof_iso["kernel"] == roof["kernel"] else None
+        kp = keccak_practical_peak()
+        if roof["bound"] == "valu" and kp:
+            # the measured ceiling of the Keccak instruction mix (half-rate v_alignbit), see DESIGN.md 7
+            roof["practical_peak"] = kp
+            roof["practical_frac"] = roof["achieved"] / kp
+            if roof["isolated_frac"] is not None:
+                roof["practical_isolated_frac"] = roof["isolated_frac"] * roof["peak"] / kp
 
     W = valu_ops(alg, args.mode)
     headline = alg == "ML-KEM-768" and args.mode == "encdec"

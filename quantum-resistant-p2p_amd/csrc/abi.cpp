@@ -188,6 +188,11 @@ static size_t scratch_for(const AlgInfo& a, size_t chunk) {
 static const AlgInfo* resolve(const char* alg) {
   const AlgInfo* a = find_alg(alg);
   if (!a) {
+    for (int i = 0; alg && i < NUNIMPL; ++i)
+      if (!strcmp(UNIMPLEMENTED[i], alg)) {
+        fail(std::string("KEM not enabled in this build: ") + alg);
+        return nullptr;
+      }
     fail(std::string("unsupported KEM: ") + (alg ? alg : "(null)"));
     return nullptr;
   }

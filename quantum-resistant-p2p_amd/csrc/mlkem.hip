@@ -20,6 +20,8 @@
 // Raw Keccak output goes to device scratch in a 64-instance tiled SoA layout
 // (word w of instance i at ((i/64)*W + w)*64 + i%64): every lane-per-instance
 // store is a fully coalesced 512-byte wave store.
+#include <algorithm>
+
 #include "keccak.cuh"
 #include "qrkem_internal.h"
 
@@ -1249,7 +1251,12 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   (void)hipMemsetAsync(v.nfix, 0, 4, st);
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
              C, (uint4*)v.xof, v.fix, v.nfix);
-  QRK_LAUNCH("k_xof_fix", st, (k_xof<K, true>), dim3(256), dim3(256), 0, st, rho, stride, n, C, (uint4*)v.xof, v.fix,
+  // one lane per listed entry in a single pass for fix-up rates up to 1/64 (~0.7 % expected):
+  // the fix-up is latency-bound (4+ sequential permutations per lane), a second grid-stride
+  // pass would double it
+  const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
+  QRK_LAUNCH("k_xof_fix", st, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, st, rho, stride, n, C,
+             (uint4*)v.xof, v.fix,
              v.nfix);
 }
 
