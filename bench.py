@@ -708,7 +708,7 @@ def main():
 
     W = valu_ops(alg, args.mode)
     headline = alg == "ML-KEM-768" and args.mode == "encdec"
-    cfg_idx = 1 if not frodo and args.mode == "encdec" else (3 if frodo else 4)
+    cfg_idx = (2 if lb >= 24 else 1) if not frodo and args.mode == "encdec" else (3 if frodo else 4)
     what = "Encaps+Decaps" if args.mode == "encdec" else "Decaps, 50% tampered (mixed)"
     result = {
         "metric": METRIC if headline else f"{alg} {'encaps+decaps' if args.mode == 'encdec' else 'decaps'}"

@@ -53,47 +53,47 @@ __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __r
   const uint32_t sc = (uint32_t)(S % cpr);
 #pragma unroll 1
   for (; rec < n; rec += srec, c += sc, (c >= cpr ? (c -= cpr, ++rec) : 0)) {
-  const uint8_t* src = in + rec * L + 12 * c;
-  const uint32_t have = L - 12 * c < 12 ? L - 12 * c : 12;
-  uint32_t w[3];
-  if (have == 12 && ((uintptr_t)src & 3) == 0) {
-    w[0] = ((const uint32_t*)src)[0], w[1] = ((const uint32_t*)src)[1], w[2] = ((const uint32_t*)src)[2];
-  } else {
+    const uint8_t* src = in + rec * L + 12 * c;
+    const uint32_t have = L - 12 * c < 12 ? L - 12 * c : 12;
+    uint32_t w[3];
+    if (have == 12 && ((uintptr_t)src & 3) == 0) {
+      w[0] = ((const uint32_t*)src)[0], w[1] = ((const uint32_t*)src)[1], w[2] = ((const uint32_t*)src)[2];
+    } else {
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
-      w[k] = ld_byte(src, 4 * k, have) | ld_byte(src, 4 * k + 1, have) << 8 | ld_byte(src, 4 * k + 2, have) << 16 |
-             ld_byte(src, 4 * k + 3, have) << 24;
-  }
-  uint32_t o[4];
+      for (int k = 0; k < 3; ++k)
+        w[k] = ld_byte(src, 4 * k, have) | ld_byte(src, 4 * k + 1, have) << 8 | ld_byte(src, 4 * k + 2, have) << 16 |
+               ld_byte(src, 4 * k + 3, have) << 24;
+    }
+    uint32_t o[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    // bytes 3g .. 3g+2 of the chunk as a big-endian 24-bit value
-    const int b = 3 * g;
-    const uint32_t b0 = (w[b >> 2] >> (8 * (b & 3))) & 0xFF;
-    const uint32_t b1 = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xFF;
-    const uint32_t b2 = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xFF;
-    const uint32_t x = b0 << 16 | b1 << 8 | b2;
-    const uint32_t c0 = *(const uint32_t*)(tb + (((x >> 11) & 0x1F80u) | tl));
-    const uint32_t c1 = *(const uint32_t*)(tb + (((x >> 5) & 0x1F80u) | tl));
-    const uint32_t c2 = *(const uint32_t*)(tb + (((x << 1) & 0x1F80u) | tl));
-    const uint32_t c3 = *(const uint32_t*)(tb + (((x << 7) & 0x1F80u) | tl));
-    uint32_t v = c0 | c1 << 8 | c2 << 16 | c3 << 24;
-    const int rem = (int)have - b;  // bytes of this group present
-    if (rem <= 0) v = 0;            // beyond the record: not stored
-    else if (rem == 1) v = (v & 0xFFFFu) | 0x3D3D0000u;
-    else if (rem == 2) v = (v & 0xFFFFFFu) | 0x3D000000u;
-    o[g] = v;
-  }
-  uint8_t* dst = out + rec * OL + 16 * c;
-  const uint32_t ngroups = (have + 2) / 3;
-  if (ngroups == 4 && ((uintptr_t)dst & 3) == 0) {
+    for (int g = 0; g < 4; ++g) {
+      // bytes 3g .. 3g+2 of the chunk as a big-endian 24-bit value
+      const int b = 3 * g;
+      const uint32_t b0 = (w[b >> 2] >> (8 * (b & 3))) & 0xFF;
+      const uint32_t b1 = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xFF;
+      const uint32_t b2 = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xFF;
+      const uint32_t x = b0 << 16 | b1 << 8 | b2;
+      const uint32_t c0 = *(const uint32_t*)(tb + (((x >> 11) & 0x1F80u) | tl));
+      const uint32_t c1 = *(const uint32_t*)(tb + (((x >> 5) & 0x1F80u) | tl));
+      const uint32_t c2 = *(const uint32_t*)(tb + (((x << 1) & 0x1F80u) | tl));
+      const uint32_t c3 = *(const uint32_t*)(tb + (((x << 7) & 0x1F80u) | tl));
+      uint32_t v = c0 | c1 << 8 | c2 << 16 | c3 << 24;
+      const int rem = (int)have - b;  // bytes of this group present
+      if (rem <= 0) v = 0;            // beyond the record: not stored
+      else if (rem == 1) v = (v & 0xFFFFu) | 0x3D3D0000u;
+      else if (rem == 2) v = (v & 0xFFFFFFu) | 0x3D000000u;
+      o[g] = v;
+    }
+    uint8_t* dst = out + rec * OL + 16 * c;
+    const uint32_t ngroups = (have + 2) / 3;
+    if (ngroups == 4 && ((uintptr_t)dst & 3) == 0) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) ((uint32_t*)dst)[g] = o[g];
-  } else {
-    for (uint32_t g = 0; g < ngroups; ++g)
+      for (int g = 0; g < 4; ++g) ((uint32_t*)dst)[g] = o[g];
+    } else {
+      for (uint32_t g = 0; g < ngroups; ++g)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) dst[4 * g + k] = (uint8_t)(o[g] >> (8 * k));
-  }
+        for (int k = 0; k < 4; ++k) dst[4 * g + k] = (uint8_t)(o[g] >> (8 * k));
+    }
   }
 }
 
@@ -118,55 +118,55 @@ __global__ __launch_bounds__(256) void k_b64_decode(size_t n, const uint8_t* __r
   const uint32_t sc = (uint32_t)(S % cpr);
 #pragma unroll 1
   for (; rec < n; rec += srec, c += sc, (c >= cpr ? (c -= cpr, ++rec) : 0)) {
-  const uint8_t* src = in + rec * IL + 16 * c;
-  const uint32_t nch = IL - 16 * c < 16 ? IL - 16 * c : 16;  // a multiple of 4
-  uint32_t w[4];
-  if (nch == 16 && ((uintptr_t)src & 3) == 0) {
+    const uint8_t* src = in + rec * IL + 16 * c;
+    const uint32_t nch = IL - 16 * c < 16 ? IL - 16 * c : 16;  // a multiple of 4
+    uint32_t w[4];
+    if (nch == 16 && ((uintptr_t)src & 3) == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = ((const uint32_t*)src)[k];
-  } else {
+      for (int k = 0; k < 4; ++k) w[k] = ((const uint32_t*)src)[k];
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      w[k] = 4 * k < (int)nch ? (uint32_t)src[4 * k] | (uint32_t)src[4 * k + 1] << 8 |
-                                    (uint32_t)src[4 * k + 2] << 16 | (uint32_t)src[4 * k + 3] << 24
-                              : 0u;
-  }
-  const uint32_t last_chunk = c + 1 == cpr;
-  const uint32_t have = last_chunk ? have_last : 12;  // output bytes of this chunk
-  uint32_t bad = 0, o[3] = {0, 0, 0};
+      for (int k = 0; k < 4; ++k)
+        w[k] = 4 * k < (int)nch ? (uint32_t)src[4 * k] | (uint32_t)src[4 * k + 1] << 8 |
+                                      (uint32_t)src[4 * k + 2] << 16 | (uint32_t)src[4 * k + 3] << 24
+                                : 0u;
+    }
+    const uint32_t last_chunk = c + 1 == cpr;
+    const uint32_t have = last_chunk ? have_last : 12;  // output bytes of this chunk
+    uint32_t bad = 0, o[3] = {0, 0, 0};
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    if (4 * g >= (int)nch) break;
-    uint32_t v = 0;
+    for (int g = 0; g < 4; ++g) {
+      if (4 * g >= (int)nch) break;
+      uint32_t v = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t ch = (w[g] >> (8 * k)) & 0xFF;
-      uint32_t d = *(const uint32_t*)(tb + (((ch << 7) & 0x3F80u) | tl)) | (ch & 0x80u);
-      // padding is legal only in the last group of the record, last `pad` positions
-      const bool is_pad_pos = last_chunk && 4 * g + 4 == (int)nch && k >= 4 - (int)pad;
-      if (is_pad_pos) {
-        bad |= ch != '=';
-        d = 0;
-      } else {
-        bad |= d >> 6;
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t ch = (w[g] >> (8 * k)) & 0xFF;
+        uint32_t d = *(const uint32_t*)(tb + (((ch << 7) & 0x3F80u) | tl)) | (ch & 0x80u);
+        // padding is legal only in the last group of the record, last `pad` positions
+        const bool is_pad_pos = last_chunk && 4 * g + 4 == (int)nch && k >= 4 - (int)pad;
+        if (is_pad_pos) {
+          bad |= ch != '=';
+          d = 0;
+        } else {
+          bad |= d >> 6;
+        }
+        v = v << 6 | (d & 63);
       }
-      v = v << 6 | (d & 63);
-    }
-    // v = 24-bit big-endian group -> bytes 3g .. 3g+2 of the chunk
+      // v = 24-bit big-endian group -> bytes 3g .. 3g+2 of the chunk
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int b = 3 * g + k;
-      o[b >> 2] |= ((v >> (16 - 8 * k)) & 0xFF) << (8 * (b & 3));
+      for (int k = 0; k < 3; ++k) {
+        const int b = 3 * g + k;
+        o[b >> 2] |= ((v >> (16 - 8 * k)) & 0xFF) << (8 * (b & 3));
+      }
     }
-  }
-  uint8_t* dst = out + rec * L + 12 * c;
-  if (have == 12 && ((uintptr_t)dst & 3) == 0) {
+    uint8_t* dst = out + rec * L + 12 * c;
+    if (have == 12 && ((uintptr_t)dst & 3) == 0) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) ((uint32_t*)dst)[k] = o[k];
-  } else {
-    for (uint32_t b = 0; b < have; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
-  }
-  if (bad && status) status[rec] = -1;
+      for (int k = 0; k < 3; ++k) ((uint32_t*)dst)[k] = o[k];
+    } else {
+      for (uint32_t b = 0; b < have; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+    }
+    if (bad && status) status[rec] = -1;
   }
 }
 
