@@ -121,32 +121,34 @@ struct Lds {
   }
 };
 
-// Two replicated tables, T0 and T2 = rot16(T0) (64 KiB): a full-round column needs one
+// Two replicated tables, T0 and T2 = rot16(T0), interleaved in one 64 KiB array: the 256 B
+// row of entry x holds T0[x] replicated 32 times (bytes 0-127) then T2[x] replicated 32 times
+// (bytes 128-255).  Lane slot s reads byte offset 256 x + 4 s (T0) or 256 x + 128 + 4 s (T2),
+// i.e. (byte r of the state word) << 8 | tl -- one v_perm_b32 per lookup, where the
+// single-table layout needs a shift and a v_and_or_b32.  A full-round column needs one
 // rotation instead of three, because rotation distributes over XOR:
 //   T0[a] ^ T1[b] ^ T2[c] ^ T3[d] = (T0[a] ^ T2[c]) ^ rot8(T0[b] ^ T2[d]).
 struct Lds2 {
-  const char* base0;
-  const char* base2;
-  uint32_t tl;
-  __device__ __forceinline__ static uint32_t off(uint32_t w, int r) {
-    return r == 0 ? (w << 7) & 0x7F80u : (w >> (8 * r - 7)) & 0x7F80u;
+  const char* base;
+  uint32_t tl0, tl2;  // 4 s and 128 + 4 s
+  __device__ __forceinline__ static uint32_t addr(uint32_t w, int r, uint32_t tl) {
+    return __builtin_amdgcn_perm(w, tl, 0x0C0C0000u | ((uint32_t)(4 + r) << 8));
   }
   __device__ __forceinline__ uint32_t t0(uint32_t w, int r) const {
-    return *(const uint32_t*)(base0 + (off(w, r) | tl));
+    return *(const uint32_t*)(base + addr(w, r, tl0));
   }
   __device__ __forceinline__ uint32_t t2(uint32_t w, int r) const {
-    return *(const uint32_t*)(base2 + (off(w, r) | tl));
+    return *(const uint32_t*)(base + addr(w, r, tl2));
   }
   // T_k[byte r of w] (generic form, used once per row)
   __device__ __forceinline__ uint32_t t(int k, uint32_t w, int r) const {
     return k == 0 ? t0(w, r) : k == 1 ? rot8(t0(w, r)) : k == 2 ? t2(w, r) : rot8(t2(w, r));
   }
 };
-__device__ __forceinline__ void fill_lds2(uint32_t* t0, uint32_t* t2, int tid, int nthreads) {
-  for (int e = tid; e < 256 * 32; e += nthreads) {
-    const uint32_t v = TAB.t0[e >> 5];
-    t0[e] = v;
-    t2[e] = rot16(v);
+__device__ __forceinline__ void fill_lds2(uint32_t* tab, int tid, int nthreads) {
+  for (int e = tid; e < 256 * 64; e += nthreads) {
+    const uint32_t v = TAB.t0[e >> 6];
+    tab[e] = (e & 32) ? rot16(v) : v;
   }
 }
 __device__ __forceinline__ void round_full2(const Lds2& L, uint32_t s[4], const uint32_t* rk) {
@@ -157,13 +159,16 @@ __device__ __forceinline__ void round_full2(const Lds2& L, uint32_t s[4], const 
 #pragma unroll
   for (int c = 0; c < 4; ++c) s[c] = o[c];
 }
+// Final round: S-box bytes sit in byte 1 of T0; two v_perm_b32 gather them.
 __device__ __forceinline__ void round_last2(const Lds2& L, uint32_t s[4], const uint32_t* rk) {
   uint32_t o[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const uint32_t a = L.t0(s[c], 0), b = L.t0(s[(c + 1) & 3], 1), d = L.t0(s[(c + 2) & 3], 2),
                    e = L.t0(s[(c + 3) & 3], 3);
-    o[c] = (((a >> 8) & 0xFFu) | (b & 0xFF00u) | (d & 0xFF0000u) | ((e << 16) & 0xFF000000u)) ^ rk[c];
+    const uint32_t lo = __builtin_amdgcn_perm(b, a, 0x0C0C0501u);  // [a.b1, b.b1, 0, 0]
+    const uint32_t hi = __builtin_amdgcn_perm(e, d, 0x05010C0Cu);  // [0, 0, d.b1, e.b1]
+    o[c] = (lo | hi) ^ rk[c];
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) s[c] = o[c];

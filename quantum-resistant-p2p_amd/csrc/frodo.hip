@@ -403,13 +403,13 @@ __global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__
 // S'A), but the 512-thread workgroup's 8 waves share one LDS-replicated T-table, and A is
 // produced 16 columns (two interleaved AES blocks) per MFMA stage.
 #ifndef QRK_AES_WAVES
-#define QRK_AES_WAVES 8
+#define QRK_AES_WAVES 16
 #endif
 #ifndef QRK_AES_COLS
 #define QRK_AES_COLS 16
 #endif
 #ifndef QRK_AES_T2
-#define QRK_AES_T2 0
+#define QRK_AES_T2 1
 #endif
 constexpr int AES_WAVES = QRK_AES_WAVES;
 constexpr int AES_COLS = QRK_AES_COLS;
@@ -418,11 +418,11 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
                                                        const int8_t* __restrict__ sp8, uint16_t* __restrict__ part) {
   using P = FP<N>;
   static_assert(N % 16 == 0 && AES_COLS % 16 == 0, "MFMA stages assume whole 16-column tiles (block pairs)");
-  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
 #if QRK_AES_T2
-  __shared__ __attribute__((aligned(16))) uint32_t tab2[256 * 32];
-  aes::fill_lds2(tab, tab2, threadIdx.x, 64 * AES_WAVES);
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry
+  aes::fill_lds2(tab, threadIdx.x, 64 * AES_WAVES);
 #else
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
   aes::fill_lds(tab, threadIdx.x, 64 * AES_WAVES);
 #endif
   __shared__ __attribute__((aligned(16))) uint16_t stg[AES_WAVES][AES_COLS * ST_PITCH];
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
   const int wv = (int)__builtin_amdgcn_readfirstlane(item % P::NWV);
   const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
 #if QRK_AES_T2
-  const aes::Lds2 L{(const char*)tab, (const char*)tab2, (uint32_t)(lane & 31) * 4u};
+  const aes::Lds2 L{(const char*)tab, (uint32_t)(lane & 31) * 4u, 128u + (uint32_t)(lane & 31) * 4u};
 #else
   const aes::Lds L{(const char*)tab, (uint32_t)(lane & 31) * 4u};
 #endif
