@@ -188,3 +188,26 @@ def test_large_batch_roundtrip_and_sample(engines):
     oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h))
     assert np.array_equal(pk_h, opk) and np.array_equal(sk_h, osk)
     assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
+
+
+def test_kat_records_through_single_shot_wrapper(golden_dir):
+    """BASELINE.json configs[0] as the reference runs it: one KEM object and one call per
+    handshake through the oqs-compatible wrapper (qrkem.oqs, the drop-in for vendor/oqs.py),
+    1024 NIST-KAT-DRBG records of ML-KEM-768, digests equal to the golden ones."""
+    import json
+    import oracle as orc
+    from qrkem import oqs
+    g = json.loads((golden_dir / "kat_mlkem.json").read_text())["ML-KEM-768"]
+    n = g["count"]
+    _, kc, ec = orc.kat_coins(n, 64, 32)
+    h = {k: hashlib.sha256() for k in ("pk", "sk", "ct", "ss")}
+    for i in range(n):
+        kem = oqs.KeyEncapsulation("ML-KEM-768")
+        pk = kem.generate_keypair_derand(kc[i].tobytes())
+        sk = kem.export_secret_key()
+        c, ss = oqs.KeyEncapsulation("ML-KEM-768").encap_secret_derand(pk, ec[i].tobytes())
+        assert oqs.KeyEncapsulation("ML-KEM-768", sk).decap_secret(c) == ss
+        for k, v in (("pk", pk), ("sk", sk), ("ct", c), ("ss", ss)):
+            h[k].update(v)
+    for k in h:
+        assert h[k].hexdigest() == g["digests"][k], k
