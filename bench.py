@@ -323,9 +323,8 @@ def bench_handshake(args, world, rank, local):
     from qrkem.handshake import SYMMETRIC_KEY_SIZE, HandshakeDriver
     from qrkem.shard import reduce_run, weak_shard
     alg = args.alg
-    if alg not in KP:
-        raise SystemExit("handshake mode: ML-KEM algorithms only in the bench")
-    lb = args.log2_batch if args.log2_batch is not None else 20
+    frodo = alg in FP
+    lb = args.log2_batch if args.log2_batch is not None else (14 if frodo else 20)
     B = 1 << lb
     drv = HandshakeDriver(alg, symmetric_name=args.symmetric, device=local, chunk=args.chunk)
     e = drv.engine
@@ -366,13 +365,13 @@ def bench_handshake(args, world, rank, local):
     disagree = int((out.agree != 1).sum().item())
     elapsed, (disagree,) = reduce_run(elapsed, [disagree], device=RED_DEVICE)
     value = B * world * args.steps / elapsed
-    W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric])
-    k = KP[alg][0]
+    W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric]) if not frodo else None
     kernels, roof = {}, None
     tot = sum(ms for ms, _ in prof.values()) or 1.0
     for name, (ms, cnt) in prof.items():
         kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot}
     if "k_xof" in prof:  # 4 SampleNTT passes per handshake (2 KeyGen, Encaps, Decaps)
+        k = KP[alg][0]
         ms, cnt = prof["k_xof"]
         ops = 4 * 3 * k * k * PERM_OPS * B * args.steps
         roof = {"kernel": "k_xof", "bound": "valu", "achieved": ops / (ms * 1e-3) / 1e12,
@@ -390,7 +389,7 @@ def bench_handshake(args, world, rank, local):
         "config": {"workload": f"{alg} batched handshake driver, 2^{lb} exchanges per GPU (SURVEY.md 8f-1)",
                    "alg": alg, "symmetric": args.symmetric, "batch_per_gpu": B, "global_batch": B * world,
                    "mean_info_bytes": info_len, "parallelism": f"index-sharded x{world} (no data-path collective)"},
-        "roofline": roof, "valu_frac_of_peak_step": value * W / VALU_PEAK, "valu_ops_per_unit": W,
+        "roofline": roof, "valu_frac_of_peak_step": value * W / VALU_PEAK if W else None, "valu_ops_per_unit": W,
         "kernels_timed_region": kernels, "checks": {"key_disagreements": disagree}, "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -398,11 +397,11 @@ def bench_handshake(args, world, rank, local):
         import oracle as orc
         threads = cpu_threads()
         take = lambda t, n: np.ascontiguousarray(t[:n].cpu().numpy())  # noqa: E731
-        cal = 512
+        cal = min(B, 64 if frodo else 512)
         t0 = time.perf_counter()
         orc.batch_handshake(alg, take(c_i, cal), take(c_r, cal), take(c_e, cal), infos[:cal], drv.key_len, threads)
         rate = cal / (time.perf_counter() - t0)
-        S = int(min(B, max(cal, (rate * 12.0) // 256 * 256)))
+        S = int(min(B, max(cal, (rate * 12.0) // 64 * 64)))
         t0 = time.perf_counter()
         pk_i, pk_r, c, key_i, key_r = orc.batch_handshake(alg, take(c_i, S), take(c_r, S), take(c_e, S), infos[:S],
                                                           drv.key_len, threads)
@@ -412,8 +411,8 @@ def bench_handshake(args, world, rank, local):
                                                                 (key_r, out.key_responder)))
         result["cpu_baseline"] = {
             "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port",
-            "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so: FIPS 203 + RFC 5869 "
-                      f"C restatement, {threads} pthreads)",
+            "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so: "
+                      f"{'FrodoKEM round 3' if frodo else 'FIPS 203'} + RFC 5869 C restatement, {threads} pthreads)",
             "sample_matches_gpu": match}
     if rank == 0:
         print(json.dumps(result))

@@ -808,44 +808,81 @@ __global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ 
   for (int k = 0; k < NBAR; ++k) bmat[(hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
 }
 
-// FrodoKEM-AES KeyGen rows: B = A S + E on VALU, lane = row, A from AES-128 (aes.cuh),
-// 256-thread workgroups sharing the LDS T-table and S^T.  KeyGen is not on the timed path.
+// FrodoKEM-AES KeyGen: column c of S as four u16 pairs (S[c][0] | S[c][1] << 16, ...), so the
+// rows kernel multiplies one A value into all 8 accumulators with 4 v_pk_mad_u16 (mod 2^16 is
+// all KeyGen needs: q | 2^16).  Written over the consumed sampler stream.
 template <int N>
-__global__ __launch_bounds__(256) void k_fr_kg_rows_aes(const uint32_t* __restrict__ prep, size_t n,
-                                                        const int8_t* __restrict__ sp8,
-                                                        const int16_t* __restrict__ e16, uint16_t* __restrict__ bmat) {
+__global__ __launch_bounds__(256) void k_fr_kg_spairs(size_t n, const int8_t* __restrict__ sp8,
+                                                      uint32_t* __restrict__ spair) {
   using P = FP<N>;
-  constexpr int WGS_PER_HS = (N + 255) / 256;
-  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
-  __shared__ int8_t st[NBAR * P::NP];
-  const uint32_t hs = __builtin_amdgcn_readfirstlane(blockIdx.x / WGS_PER_HS);
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t hs = t / N;
+  const int c = (int)(t % N);
   if (hs >= n) return;
-  const int r = (int)(blockIdx.x % WGS_PER_HS) * 256 + threadIdx.x;
-  aes::fill_lds(tab, threadIdx.x, 256);
-  for (int t = threadIdx.x; t < NBAR * P::NP; t += 256) st[t] = sp8[(size_t)hs * NBAR * P::NP + t];
+  const int8_t* s = sp8 + hs * NBAR * P::NP + c;
+  uint4 o;
+  o.x = (uint32_t)(uint16_t)(int16_t)s[0 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[1 * P::NP] << 16;
+  o.y = (uint32_t)(uint16_t)(int16_t)s[2 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[3 * P::NP] << 16;
+  o.z = (uint32_t)(uint16_t)(int16_t)s[4 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[5 * P::NP] << 16;
+  o.w = (uint32_t)(uint16_t)(int16_t)s[6 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[7 * P::NP] << 16;
+  ((uint4*)spair)[hs * N + c] = o;
+}
+
+// Workgroup size of the AES KeyGen rows kernel: all rows of a handshake in as few
+// workgroups as possible (at most 1024 threads), whole waves.
+template <int N>
+constexpr int kg_wgs() { return (N + 1023) / 1024; }
+template <int N>
+constexpr int kg_threads() { return ((N + kg_wgs<N>() - 1) / kg_wgs<N>() + 63) / 64 * 64; }
+
+// FrodoKEM-AES KeyGen rows: B = A S + E (mod 2^16), lane = row, A from AES-128 with the
+// two-table LDS layout of k_fr_gen_mm_aes (two blocks per iteration), S from the uniform
+// pair table (scalar loads), 4 packed 16-bit multiply-adds per A value.  Not on the timed path
+// of encaps/decaps, but twice per exchange in the handshake driver.
+template <int N>
+__global__ __launch_bounds__(kg_threads<N>()) void k_fr_kg_rows_aes(const uint32_t* __restrict__ prep, size_t n,
+                                                                    const uint32_t* __restrict__ spair,
+                                                                    const int16_t* __restrict__ e16,
+                                                                    uint16_t* __restrict__ bmat) {
+  using P = FP<N>;
+  constexpr int T = kg_threads<N>();
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];
+  const uint32_t hs = __builtin_amdgcn_readfirstlane(blockIdx.x / kg_wgs<N>());
+  if (hs >= n) return;
+  const int r = (int)(blockIdx.x % kg_wgs<N>()) * T + threadIdx.x;
+  aes::fill_lds2(tab, threadIdx.x, T);
   __syncthreads();
   if (r >= N) return;
   const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
-  const aes::Lds L{(const char*)tab, (uint32_t)(threadIdx.x & 31) * 4u};
+  const aes::Lds2 L{(const char*)tab, (uint32_t)(threadIdx.x & 31) * 4u, 128u + (uint32_t)(threadIdx.x & 31) * 4u};
   uint32_t lp[4];
   aes::row_part(L, hp, (uint32_t)r, lp);
-  uint32_t acc[NBAR];
-#pragma unroll
-  for (int k = 0; k < NBAR; ++k) acc[k] = (uint32_t)(int32_t)e16[((size_t)hs * N + r) * NBAR + k];
+  u16x2 acc[4];
+  {
+    const uint4 e = *(const uint4*)(e16 + ((size_t)hs * N + r) * NBAR);  // E[r][0..7], int16 LE
+    acc[0] = __builtin_bit_cast(u16x2, e.x), acc[1] = __builtin_bit_cast(u16x2, e.y);
+    acc[2] = __builtin_bit_cast(u16x2, e.z), acc[3] = __builtin_bit_cast(u16x2, e.w);
+  }
+  const uint32_t* sp = spair + (size_t)hs * N * 4;
 #pragma unroll 1
-  for (int jb = 0; jb < N / 8; ++jb) {
+  for (int jb = 0; jb < N / 8; jb += 2) {
     const uint32_t* u = hp + aes::PREP_HDR + 4 * jb;
     uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
-    aes::rounds_3_10(L, z, hp);
+    uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
+    aes::rounds_3_10_x2(L, z, w, hp);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t v = (z[e >> 1] >> (16 * (e & 1))) & 0xFFFF;
+    for (int e = 0; e < 16; ++e) {
+      const uint32_t x = e < 8 ? z[e >> 1] : w[(e - 8) >> 1];
+      const u16x2 vv = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(x, x, (e & 1) ? 0x03020302u : 0x01000100u));
+      const uint32_t* s4 = sp + (size_t)(8 * jb + e) * 4;
 #pragma unroll
-      for (int k = 0; k < NBAR; ++k) acc[k] += v * (uint32_t)(int32_t)st[k * P::NP + 8 * jb + e];
+      for (int q = 0; q < 4; ++q) acc[q] = vv * __builtin_bit_cast(u16x2, s4[q]) + acc[q];
     }
   }
-#pragma unroll
-  for (int k = 0; k < NBAR; ++k) bmat[((size_t)hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
+  const uint32_t m = P::QMASK | (P::QMASK << 16);
+  *(uint4*)(bmat + ((size_t)hs * N + r) * NBAR) =
+      make_uint4(__builtin_bit_cast(uint32_t, acc[0]) & m, __builtin_bit_cast(uint32_t, acc[1]) & m,
+                 __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
 }
 
 // pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh.  One 256-thread workgroup
@@ -981,8 +1018,10 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   if constexpr (AES) {
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
                (size_t)P::PK, n, v.aesp);
-    QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * ((N + 255) / 256))), dim3(256), 0,
-               st, v.aesp, n, v.sp8, v.ep16, v.part);
+    uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
+    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
+    QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())), dim3(kg_threads<N>()),
+               0, st, v.aesp, n, spair, v.ep16, v.part);
   } else {
     QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
                v.sp8, v.ep16, v.part);
