@@ -757,58 +757,7 @@ __global__ __launch_bounds__(256) void k_fr_kg_front(const uint8_t* __restrict__
   }
 }
 
-// B = A S + E (mod q) on VALU: lane r generates row r of A and dots it with the
-// 8 rows of S^T (staged in LDS).  KeyGen is not on the timed path.
-template <int N>
-__global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ pk, size_t n,
-                                                    const int8_t* __restrict__ sp8, const int16_t* __restrict__ e16,
-                                                    uint16_t* __restrict__ bmat) {
-  using P = FP<N>;
-  constexpr int WGS_PER_HS = P::NP / 128;
-  __shared__ int8_t st[NBAR * P::NP];
-  const size_t hs = blockIdx.x / WGS_PER_HS;
-  if (hs >= n) return;
-  const int r = (int)(blockIdx.x % WGS_PER_HS) * 128 + threadIdx.x;
-  for (int t = threadIdx.x; t < NBAR * P::NP; t += 128) st[t] = sp8[hs * NBAR * P::NP + t];
-  __syncthreads();
-  if (r >= N) return;
-  const uint8_t* sa = pk + hs * P::PK;
-  uint64_t in[3];
-  {
-    const uint64_t s0 = ((const uint64_t*)sa)[0], s1 = ((const uint64_t*)sa)[1];
-    in[0] = (uint64_t)(r & 0xFFFF) | (s0 << 16);
-    in[1] = (s0 >> 48) | (s1 << 16);
-    in[2] = s1 >> 48;
-  }
-  KState s;
-  kzero(s);
-  absorb_short<21, 3>(s, in, 18);
-  uint32_t acc[NBAR];
-#pragma unroll
-  for (int k = 0; k < NBAR; ++k) acc[k] = (uint32_t)(int32_t)e16[(hs * N + r) * NBAR + k];
-#pragma unroll 1
-  for (int b = 0; b < P::A_BLOCKS; ++b) {
-    if (b) keccak_f(s);
-    const int c0 = 84 * b;
-#pragma unroll
-    for (int w = 0; w < 21; ++w) {
-      const uint32_t lo = s.a[w].lo, hi = s.a[w].hi;
-      const uint32_t v[4] = {lo & 0xFFFF, lo >> 16, hi & 0xFFFF, hi >> 16};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = c0 + 4 * w + e;
-        if (c < N) {
-#pragma unroll
-          for (int k = 0; k < NBAR; ++k) acc[k] += v[e] * (uint32_t)(int32_t)st[k * P::NP + c];
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NBAR; ++k) bmat[(hs * N + r) * NBAR + k] = (uint16_t)(acc[k] & P::QMASK);
-}
-
-// FrodoKEM-AES KeyGen: column c of S as four u16 pairs (S[c][0] | S[c][1] << 16, ...), so the
+// KeyGen: column c of S as four u16 pairs (S[c][0] | S[c][1] << 16, ...), so the
 // rows kernel multiplies one A value into all 8 accumulators with 4 v_pk_mad_u16 (mod 2^16 is
 // all KeyGen needs: q | 2^16).  Written over the consumed sampler stream.
 template <int N>
@@ -826,6 +775,62 @@ __global__ __launch_bounds__(256) void k_fr_kg_spairs(size_t n, const int8_t* __
   o.z = (uint32_t)(uint16_t)(int16_t)s[4 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[5 * P::NP] << 16;
   o.w = (uint32_t)(uint16_t)(int16_t)s[6 * P::NP] | (uint32_t)(uint16_t)(int16_t)s[7 * P::NP] << 16;
   ((uint4*)spair)[hs * N + c] = o;
+}
+
+// B = A S + E (mod 2^16) on VALU: lane r generates row r of A (SHAKE128) and multiplies each
+// value into the 8 accumulators with 4 v_pk_mad_u16 against the uniform S-pair table.
+// KeyGen is not on the encaps/decaps timed path (twice per exchange in the handshake driver).
+template <int N>
+__global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ pk, size_t n,
+                                                    const uint32_t* __restrict__ spair,
+                                                    const int16_t* __restrict__ e16, uint16_t* __restrict__ bmat) {
+  using P = FP<N>;
+  constexpr int WGS_PER_HS = P::NP / 128;
+  const uint32_t hs = __builtin_amdgcn_readfirstlane(blockIdx.x / WGS_PER_HS);
+  if (hs >= n) return;
+  const int r = (int)(blockIdx.x % WGS_PER_HS) * 128 + threadIdx.x;
+  if (r >= N) return;
+  const uint8_t* sa = pk + (size_t)hs * P::PK;
+  uint64_t in[3];
+  {
+    const uint64_t s0 = ((const uint64_t*)sa)[0], s1 = ((const uint64_t*)sa)[1];
+    in[0] = (uint64_t)(r & 0xFFFF) | (s0 << 16);
+    in[1] = (s0 >> 48) | (s1 << 16);
+    in[2] = s1 >> 48;
+  }
+  KState s;
+  kzero(s);
+  absorb_short<21, 3>(s, in, 18);
+  u16x2 acc[4];
+  {
+    const uint4 e = *(const uint4*)(e16 + ((size_t)hs * N + r) * NBAR);  // E[r][0..7], int16 LE
+    acc[0] = __builtin_bit_cast(u16x2, e.x), acc[1] = __builtin_bit_cast(u16x2, e.y);
+    acc[2] = __builtin_bit_cast(u16x2, e.z), acc[3] = __builtin_bit_cast(u16x2, e.w);
+  }
+  const uint32_t* sp = spair + (size_t)hs * N * 4;
+#pragma unroll 1
+  for (int b = 0; b < P::A_BLOCKS; ++b) {
+    if (b) keccak_f(s);
+    const int c0 = 84 * b;
+#pragma unroll
+    for (int w = 0; w < 21; ++w) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = c0 + 4 * w + e;
+        if (c < N) {
+          const uint32_t x = (e < 2) ? s.a[w].lo : s.a[w].hi;
+          const u16x2 vv = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(x, x, (e & 1) ? 0x03020302u : 0x01000100u));
+          const uint32_t* s4 = sp + (size_t)c * 4;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q] = vv * __builtin_bit_cast(u16x2, s4[q]) + acc[q];
+        }
+      }
+    }
+  }
+  const uint32_t m = P::QMASK | (P::QMASK << 16);
+  *(uint4*)(bmat + ((size_t)hs * N + r) * NBAR) =
+      make_uint4(__builtin_bit_cast(uint32_t, acc[0]) & m, __builtin_bit_cast(uint32_t, acc[1]) & m,
+                 __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
 }
 
 // Workgroup size of the AES KeyGen rows kernel: all rows of a handshake in as few
@@ -1015,16 +1020,16 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   // S^T -> sp8 ([8][NP] int8), E -> ep16 as [N][8]
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
+  uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
+  QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
   if constexpr (AES) {
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
                (size_t)P::PK, n, v.aesp);
-    uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
-    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
     QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())), dim3(kg_threads<N>()),
                0, st, v.aesp, n, spair, v.ep16, v.part);
   } else {
     QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
-               v.sp8, v.ep16, v.part);
+               spair, v.ep16, v.part);
   }
   QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(256), 0, st, n, v.part, v.sp8, pk, sk);
   QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, n, sk);
