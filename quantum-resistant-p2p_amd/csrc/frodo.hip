@@ -411,6 +411,9 @@ __global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__
 #ifndef QRK_AES_T2
 #define QRK_AES_T2 1
 #endif
+#ifndef QRK_AES_BSTG
+#define QRK_AES_BSTG 1
+#endif
 constexpr int AES_WAVES = QRK_AES_WAVES;
 constexpr int AES_COLS = QRK_AES_COLS;
 template <int N>
@@ -425,7 +428,13 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
   __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
   aes::fill_lds(tab, threadIdx.x, 64 * AES_WAVES);
 #endif
+#if QRK_AES_BSTG
+  // one byte per (column, row): lo limbs, MFMA, then hi limbs in the same 1 KiB, so 16 waves
+  // fit twice per CU beside the 64 KiB table (2 x 80 KiB)
+  __shared__ __attribute__((aligned(16))) uint8_t stb[AES_WAVES][16 * 64];
+#else
   __shared__ __attribute__((aligned(16))) uint16_t stg[AES_WAVES][AES_COLS * ST_PITCH];
+#endif
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t item = (uint32_t)blockIdx.x * AES_WAVES + (uint32_t)wave;
@@ -444,8 +453,47 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
   if (kq < NBAR) y = *(const v4i*)(sp8 + ((size_t)hs * NBAR + kq) * P::NP + wv * 64 + ks);  // zero past row N
   uint32_t lp[4];
   aes::row_part(L, hp, (uint32_t)r, lp);
-  uint16_t* st = stg[wave];
   uint16_t* prt = part + ((size_t)hs * P::NWV + wv) * NBAR * N;
+#if QRK_AES_BSTG
+  static_assert(AES_COLS == 16, "byte staging holds one 16-column tile");
+  uint8_t* sb = stb[wave];
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += 16) {
+    const uint32_t* u = hp + aes::PREP_HDR + 4 * (c0 >> 3);
+    uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
+    uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
+    aes::rounds_3_10_x2(L, z, w, hp);
+    const v4i zr = {0, 0, 0, 0};
+    v4i d[2];
+#pragma unroll
+    for (int limb = 0; limb < 2; ++limb) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // word q = values 2q, 2q+1 (little-endian u16)
+        const uint32_t x = q < 4 ? z[q] : w[q - 4];
+        const uint32_t y8 = limb ? add80(x) >> 8 : x;  // lo = a & 0xFF, hi = (a + 128) >> 8
+        sb[(2 * q) * 64 + lane] = (uint8_t)y8;
+        sb[(2 * q + 1) * 64 + lane] = (uint8_t)(y8 >> 16);
+      }
+      wsync();
+      const v4i xv = *(const v4i*)(sb + kq * 64 + ks);  // rows ks .. ks+15 of column kq
+      d[limb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, y, zr, 0, 0, 0);
+      wsync();
+    }
+    const int cl = 4 * (lane >> 4);
+    if (kq < NBAR) {
+      uint32_t v[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)d[0][g] + ((uint32_t)d[1][g] << 8)) & 0xFFFFu;
+      *(uint2*)(prt + kq * N + c0 + cl) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+    }
+  }
+#else
+  uint16_t* st = stg[wave];
 #pragma unroll 1
   for (int c0 = 0; c0 < N; c0 += AES_COLS) {
     const int nc = (N - c0) < AES_COLS ? (N - c0) : AES_COLS;
@@ -497,6 +545,7 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+#endif
 }
 
 // LOGQ-bit MSB-first bit-field reads / writes
