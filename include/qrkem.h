@@ -132,6 +132,12 @@ int qrk_kem_encaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ct, u
                          const uint8_t *pk, const uint8_t *coins, int32_t *status, void *stream);
 int qrk_kem_decaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
                          const uint8_t *sk, void *stream);
+/* Decaps with a per-record return code (device int32[n]): HQC writes -1 where the
+ * re-encryption check fails -- the OQS_ERROR liboqs's HQC decaps returns, which makes the
+ * reference's KeyEncapsulation.decap_secret raise (oqs.py:372-380); ss_i = K(sigma || ct_i)
+ * is written either way.  ML-KEM and FrodoKEM (implicit rejection, return 0) write 0. */
+int qrk_kem_decaps_batch_status(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
+                                const uint8_t *sk, int32_t *status, void *stream);
 
 /* Same, with host buffers (synchronous; copies through pinned staging). */
 int qrk_kem_keypair_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *pk, uint8_t *sk,
@@ -140,6 +146,8 @@ int qrk_kem_encaps_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *
                               const uint8_t *pk, const uint8_t *coins, int32_t *status);
 int qrk_kem_decaps_batch_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
                               const uint8_t *sk);
+int qrk_kem_decaps_batch_status_host(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ss, const uint8_t *ct,
+                                     const uint8_t *sk, int32_t *status);
 
 /* Bench inputs generated on device: out_i = SHAKE256("qrk-bench"||LE64(seed)||LE64(first+i), len),
  * len a multiple of 8, <= 136.  Device pointer. */

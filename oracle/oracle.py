@@ -51,6 +51,7 @@ def lib() -> ct.CDLL:
         L.orc_encaps.argtypes = [ct.c_char_p, P, P, P, P]
         L.orc_decaps.argtypes = [ct.c_char_p, P, P, P]
         L.orc_batch.argtypes = [ct.c_char_p, ct.c_int, ct.c_size_t, ct.c_int, P, P, P, P]
+        L.orc_batch_status.argtypes = [ct.c_char_p, ct.c_int, ct.c_size_t, ct.c_int, P, P, P, P, P]
         L.orc_bench_coins.argtypes = [P, ct.c_size_t, ct.c_size_t, ct.c_uint64, ct.c_uint64]
         L.orc_bench_coins.restype = None
         L.orc_hash.argtypes = [ct.c_int, P, ct.c_size_t, P, ct.c_size_t]
@@ -93,12 +94,20 @@ def encaps(alg: str, pk: bytes, coins: bytes) -> tuple[bytes, bytes]:
     return c.raw, ss.raw
 
 
-def decaps(alg: str, sk: bytes, c: bytes) -> bytes:
+def decaps_rc(alg: str, sk: bytes, c: bytes) -> tuple[bytes, int]:
+    """(ss, rc).  HQC: rc = -1 when the re-encryption check fails (ss still written),
+    the OQS_KEM_decaps return liboqs gives; ML-KEM / FrodoKEM always return 0."""
     s = sizes(alg)
     ss = ct.create_string_buffer(s["ss"])
-    if lib().orc_decaps(alg.encode(), ss, _buf(c), _buf(sk)) != 0:
+    rc = lib().orc_decaps(alg.encode(), ss, _buf(c), _buf(sk))
+    return ss.raw, int(rc)
+
+
+def decaps(alg: str, sk: bytes, c: bytes) -> bytes:
+    ss, rc = decaps_rc(alg, sk, c)
+    if rc != 0:
         raise RuntimeError("oracle decaps failed")
-    return ss.raw
+    return ss
 
 
 def _ptr(a: np.ndarray):
@@ -130,15 +139,18 @@ def batch_encaps(alg: str, pk: np.ndarray, coins: np.ndarray, threads: int = 0):
     return c, ss
 
 
-def batch_decaps(alg: str, sk: np.ndarray, c: np.ndarray, threads: int = 0) -> np.ndarray:
+def batch_decaps(alg: str, sk: np.ndarray, c: np.ndarray, threads: int = 0, with_status: bool = False):
+    """ss [n, ss]; with_status: (ss, status int32 [n]) with each record's decaps return code."""
     s = sizes(alg)
     n = sk.shape[0]
     ss = np.zeros((n, s["ss"]), np.uint8)
-    rc = lib().orc_batch(alg.encode(), 2, n, threads or os.cpu_count(), _ptr(ss), None,
-                         _ptr(np.ascontiguousarray(c)), _ptr(np.ascontiguousarray(sk)))
+    st = np.zeros(n, np.int32)
+    rc = lib().orc_batch_status(alg.encode(), 2, n, threads or os.cpu_count(), _ptr(ss), None,
+                                _ptr(np.ascontiguousarray(c)), _ptr(np.ascontiguousarray(sk)),
+                                _ptr(st) if with_status else None)
     if rc:
         raise RuntimeError("oracle batch decaps failed")
-    return ss
+    return (ss, st) if with_status else ss
 
 
 def bench_coins(n: int, length: int, seed: int, first_index: int = 0) -> np.ndarray:

@@ -20,8 +20,15 @@
 #include "mlkem.h"
 
 static int is_mlkem(const char *alg) { return !strncmp(alg, "ML-KEM-", 7); }
+static int is_hqc(const char *alg) { return !strncmp(alg, "HQC-", 4); }
+
+int orc_hqc_sizes(const char *alg, size_t out[6]);
+int orc_hqc_keypair_derand(const char *alg, uint8_t *pk, uint8_t *sk, const uint8_t *coins);
+int orc_hqc_encaps_derand(const char *alg, uint8_t *ct, uint8_t *ss, const uint8_t *pk, const uint8_t *coins);
+int orc_hqc_decaps(const char *alg, uint8_t *ss, const uint8_t *ct, const uint8_t *sk);
 
 int orc_sizes(const char *alg, size_t out[6]) {
+  if (is_hqc(alg)) return orc_hqc_sizes(alg, out);
   if (is_mlkem(alg)) {
     if (orc_mlkem_sizes(alg, &out[0], &out[1], &out[2], &out[3])) return -1;
     out[4] = 64;
@@ -32,14 +39,18 @@ int orc_sizes(const char *alg, size_t out[6]) {
 }
 
 int orc_keypair(const char *alg, uint8_t *pk, uint8_t *sk, const uint8_t *coins) {
+  if (is_hqc(alg)) return orc_hqc_keypair_derand(alg, pk, sk, coins);
   return is_mlkem(alg) ? orc_mlkem_keypair_derand(alg, pk, sk, coins)
                        : orc_frodo_keypair_derand(alg, pk, sk, coins);
 }
 int orc_encaps(const char *alg, uint8_t *ct, uint8_t *ss, const uint8_t *pk, const uint8_t *coins) {
+  if (is_hqc(alg)) return orc_hqc_encaps_derand(alg, ct, ss, pk, coins);
   return is_mlkem(alg) ? orc_mlkem_encaps_derand(alg, ct, ss, pk, coins)
                        : orc_frodo_encaps_derand(alg, ct, ss, pk, coins);
 }
+/* HQC returns -1 when the re-encryption check fails (ss is still written), as liboqs does */
 int orc_decaps(const char *alg, uint8_t *ss, const uint8_t *ct, const uint8_t *sk) {
+  if (is_hqc(alg)) return orc_hqc_decaps(alg, ss, ct, sk);
   return is_mlkem(alg) ? orc_mlkem_decaps(alg, ss, ct, sk) : orc_frodo_decaps(alg, ss, ct, sk);
 }
 
@@ -53,6 +64,7 @@ typedef struct {
   uint8_t *a, *b;
   const uint8_t *c, *d;
   size_t sz[6];
+  int32_t *status; /* optional per-record return code */
   int rc;
 } job;
 
@@ -74,15 +86,24 @@ static void *run_job(void *arg) {
         rc = orc_decaps(j->alg, j->a + i * SS, j->c + i * CT, j->d + i * SK);
         break;
     }
-    if (rc) j->rc = rc;
+    if (j->status) j->status[i] = rc;
+    else if (rc) j->rc = rc;
   }
   return NULL;
 }
 
 /* op: 0 keypair(pk=a, sk=b, coins=c); 1 encaps(ct=a, ss=b, pk=c, coins=d);
  *     2 decaps(ss=a, ct=c, sk=d).  Returns 0 or -1. */
+int orc_batch_status(const char *alg, int op, size_t n, int nthreads, uint8_t *a, uint8_t *b,
+                     const uint8_t *c, const uint8_t *d, int32_t *status);
 int orc_batch(const char *alg, int op, size_t n, int nthreads, uint8_t *a, uint8_t *b,
               const uint8_t *c, const uint8_t *d) {
+  return orc_batch_status(alg, op, n, nthreads, a, b, c, d, NULL);
+}
+
+/* as orc_batch; with status != NULL each record's return code lands in status[i] instead */
+int orc_batch_status(const char *alg, int op, size_t n, int nthreads, uint8_t *a, uint8_t *b,
+                     const uint8_t *c, const uint8_t *d, int32_t *status) {
   size_t sz[6];
   if (orc_sizes(alg, sz)) return -1;
   if (nthreads < 1) nthreads = 1;
@@ -95,6 +116,7 @@ int orc_batch(const char *alg, int op, size_t n, int nthreads, uint8_t *a, uint8
     jobs[t].lo = n * t / nthreads;
     jobs[t].hi = n * (t + 1) / nthreads;
     jobs[t].a = a, jobs[t].b = b, jobs[t].c = c, jobs[t].d = d;
+    jobs[t].status = status;
     memcpy(jobs[t].sz, sz, sizeof sz);
     pthread_create(&th[t], NULL, run_job, &jobs[t]);
   }

@@ -32,15 +32,18 @@ static AlgInfo ALGS[] = {
     {"FrodoKEM-976-SHAKE", Family::FRODO, 3, 976, 15632, 31296, 15744, 24, 64, 24, false, true},
     {"FrodoKEM-1344-AES", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, true, true},
     {"FrodoKEM-1344-SHAKE", Family::FRODO, 5, 1344, 21520, 43088, 21632, 32, 80, 32, false, true},
+    {"HQC-128", Family::HQC, 1, 128, 2249, 2305, 4433, 64, 96, 32, false, true},
+    {"HQC-192", Family::HQC, 3, 192, 4522, 4586, 8978, 64, 104, 40, false, true},
+    {"HQC-256", Family::HQC, 5, 256, 7245, 7317, 14421, 64, 112, 48, false, true},
 };
 static const int NALG = (int)(sizeof(ALGS) / sizeof(ALGS[0]));
 
 // Names liboqs supports that this engine does not implement (listed so that
 // OQS_KEM_alg_is_enabled answers 0 rather than the name being unknown, the
 // distinction oqs.py:265-269 draws between MechanismNotEnabledError and
-// MechanismNotSupportedError).
-static const char* UNIMPLEMENTED[] = {"HQC-128", "HQC-192", "HQC-256"};
-static const int NUNIMPL = 3;
+// MechanismNotSupportedError).  Every KEM the reference selects is implemented.
+static const char* UNIMPLEMENTED[] = {nullptr};
+static const int NUNIMPL = 0;
 
 const AlgInfo* find_alg(const char* name) {
   if (!name) return nullptr;
@@ -182,7 +185,11 @@ static int os_random(uint8_t* out, size_t n) {
 }
 
 static size_t scratch_for(const AlgInfo& a, size_t chunk) {
-  return a.family == Family::MLKEM ? mlkem_scratch_bytes(a, chunk) : frodo_scratch_bytes(a, chunk);
+  switch (a.family) {
+    case Family::MLKEM: return mlkem_scratch_bytes(a, chunk);
+    case Family::FRODO: return frodo_scratch_bytes(a, chunk);
+    default: return hqc_scratch_bytes(a, chunk);
+  }
 }
 
 static const AlgInfo* resolve(const char* alg) {
@@ -205,11 +212,12 @@ static const AlgInfo* resolve(const char* alg) {
 
 enum class Op { KEYPAIR, ENCAPS, DECAPS };
 
-// FrodoKEM scratch is 0.14-0.53 MB per handshake: its chunk is capped so scratch stays near 8 GiB
+// FrodoKEM scratch is 0.14-0.53 MB per handshake, HQC's 9-24 KB: their chunks are capped so
+// scratch stays near 8 GiB
 static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
   size_t cap = ctx->chunk;
-  if (a.family == Family::FRODO) {
-    const size_t per_hs = frodo_scratch_bytes(a, 1024) / 1024 + 1;
+  if (a.family != Family::MLKEM) {
+    const size_t per_hs = scratch_for(a, 1024) / 1024 + 1;
     cap = std::min(cap, std::max<size_t>(4096, ((size_t)8 << 30) / per_hs / 64 * 64));
   }
   return cap;
@@ -273,7 +281,26 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
                            status ? status + off : nullptr, ctx->scratch, S);
           break;
         case Op::DECAPS:
-          e = mlkem_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
+          if (status) e = hipMemsetAsync(status + off, 0, m * sizeof(int32_t), st);
+          if (e == hipSuccess)
+            e = mlkem_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
+          break;
+      }
+    } else if (a.family == Family::HQC) {
+      switch (op) {
+        case Op::KEYPAIR:
+          e = hqc_keypair(a, m, o1 + off * a.pk, o2 + off * a.sk, coins + off * clen, ctx->scratch, S);
+          break;
+        case Op::ENCAPS:
+          // HQC encapsulation has no public-key validity check: status is always 0
+          if (status) e = hipMemsetAsync(status + off, 0, m * sizeof(int32_t), st);
+          if (e == hipSuccess)
+            e = hqc_encaps(a, m, o1 + off * a.ct, o2 + off * a.ss, i1 + off * a.pk, coins + off * clen, ctx->scratch,
+                           S);
+          break;
+        case Op::DECAPS:
+          e = hqc_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, status ? status + off : nullptr,
+                         ctx->scratch, S);
           break;
       }
     } else {
@@ -289,7 +316,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
                              ctx->scratch, S);
           break;
         case Op::DECAPS:
-          e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
+          if (status) e = hipMemsetAsync(status + off, 0, m * sizeof(int32_t), st);
+          if (e == hipSuccess)
+            e = frodo_decaps(a, m, o1 + off * a.ss, i1 + off * a.ct, i2 + off * a.sk, ctx->scratch, S);
           break;
       }
     }
@@ -367,8 +396,12 @@ static OQS_STATUS single(const AlgInfo& a, Op op, uint8_t* o1, uint8_t* o2, cons
   qrk_ctx* ctx = default_ctx();
   std::lock_guard<std::mutex> lk(ctx->mu);
   int32_t status = 0;
-  int rc = run_batch_host(ctx, a, op, 1, o1, o2, i1, i2, op == Op::ENCAPS ? &status : nullptr);
-  if (rc == 0 && status != 0) rc = fail("encapsulation key failed the FIPS 203 modulus check");
+  int rc = run_batch_host(ctx, a, op, 1, o1, o2, i1, i2, op == Op::KEYPAIR ? nullptr : &status);
+  // ML-KEM encaps: the FIPS 203 modulus check; HQC decaps: liboqs returns OQS_ERROR when the
+  // re-encryption check fails (the shared secret K(sigma || ct) is still written)
+  if (rc == 0 && status != 0)
+    rc = fail(op == Op::ENCAPS ? "encapsulation key failed the FIPS 203 modulus check"
+                               : "ciphertext rejected by the re-encryption check");
   return rc == 0 ? OQS_SUCCESS : OQS_ERROR;
 }
 
@@ -388,7 +421,7 @@ static OQS_STATUS cb_decaps(uint8_t* ss, const uint8_t* ct, const uint8_t* sk) {
 
 template <int I>
 static void fill_cbs(OQS_KEM* k, int idx) {
-  if constexpr (I < 9) {
+  if constexpr (I < (int)(sizeof(ALGS) / sizeof(ALGS[0]))) {
     if (idx == I) {
       k->keypair = cb_keypair<I>;
       k->encaps = cb_encaps<I>;
@@ -425,7 +458,9 @@ OQS_KEM* OQS_KEM_new(const char* method_name) {
   OQS_KEM* k = (OQS_KEM*)calloc(1, sizeof(OQS_KEM));
   if (!k) return nullptr;
   k->method_name = a->name;
-  k->alg_version = a->family == Family::MLKEM ? "FIPS203 (qrkem gfx950)" : "FrodoKEM round 3 (qrkem gfx950)";
+  k->alg_version = a->family == Family::MLKEM   ? "FIPS203 (qrkem gfx950)"
+                   : a->family == Family::FRODO ? "FrodoKEM round 3 (qrkem gfx950)"
+                                                : "HQC 2023-04-30 (qrkem gfx950)";
   k->claimed_nist_level = (uint8_t)a->level;
   k->ind_cca = true;
   k->length_public_key = a->pk;
@@ -609,6 +644,11 @@ int qrk_kem_decaps_batch(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ss, c
   QRK_RESOLVE(ctx, alg);
   return run_batch(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, nullptr, (hipStream_t)stream);
 }
+int qrk_kem_decaps_batch_status(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ss, const uint8_t* ct,
+                                const uint8_t* sk, int32_t* status, void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, status, (hipStream_t)stream);
+}
 int qrk_kem_keypair_batch_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* pk, uint8_t* sk,
                                const uint8_t* coins) {
   QRK_RESOLVE(ctx, alg);
@@ -623,6 +663,11 @@ int qrk_kem_decaps_batch_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* 
                               const uint8_t* sk) {
   QRK_RESOLVE(ctx, alg);
   return run_batch_host(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, nullptr);
+}
+int qrk_kem_decaps_batch_status_host(qrk_ctx* ctx, const char* alg, size_t n, uint8_t* ss, const uint8_t* ct,
+                                     const uint8_t* sk, int32_t* status) {
+  QRK_RESOLVE(ctx, alg);
+  return run_batch_host(ctx, *a, Op::DECAPS, n, ss, nullptr, ct, sk, status);
 }
 
 int qrk_bench_coins(qrk_ctx* ctx, size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, void* stream) {

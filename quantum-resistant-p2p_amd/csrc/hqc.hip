@@ -1,0 +1,796 @@
+// HQC-128/192/256 (round-4 submission, version 2023-04-30) KeyGen / Encaps / Decaps for gfx950.
+//
+// Replaces liboqs's HQC behind OQS_KEM_keypair/encaps/decaps, which the reference reaches
+// from HQCKeyExchange (quantum_resistant_p2p/crypto/key_exchange.py:189-309) through
+// vendor/oqs.py:318,348,372.  Conventions are restated in oracle/py/hqc_spec.py.
+//
+// Kernels (C = chunk of handshakes):
+//   k_hqc_kg_expand   lane / hs   SE(sk_seed) -> x, y random words; SE(pk_seed) -> h stream
+//   k_hqc_enc_expand  lane / hs   theta = G(m || pk[0:80] || salt); SE(theta) -> r1, r2, e words; SE(pk_seed) -> h
+//   k_hqc_dec_expand  lane / hs   SE(sk_seed) -> x, y words (decryption uses y)
+//   k_hqc_kg_mul      WG / hs     s = x + y h; pk = pk_seed || s; sk = sk_seed || sigma || pk
+//   k_hqc_enc_mul     WG / hs     u = r1 + r2 h, v = C.encode(m) + r2 s + e (truncated); ct; K-hash message
+//                                 (REENC: the same re-encryption inside Decaps, compared with the received ct)
+//   k_hqc_decode      WG / hs     v - u y, duplicated RM(1,7) decoding (wave-wide Hadamard transform),
+//                                 RS decoding (syndromes, Berlekamp-Massey, Chien, Forney) -> m'
+//   k_hqc_hash        lane / hs   ss = SHAKE256(m || u || v || 0x05)
+//
+// The sparse-dense products in F2[X]/(X^n - 1) run one workgroup (256 threads) per handshake.
+// The dense operand b is kept in LDS "doubled": D = b_raw ^ (clean(b) << n) as 32-bit words,
+// so that bit p of X^k b is bit p + n - k of D and every output word is one funnel shift
+// (v_alignbit) of two consecutive D words; the shift is uniform per position k.  Thread t owns
+// WPT consecutive output words.  b_raw keeps the bits above X^(n-1) a malformed pk/ct carries,
+// which reproduces the reference's single-fold reduction exactly (oracle/src/hqc.c mul_sparse).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "keccak.cuh"
+#include "qrkem_internal.h"
+
+namespace qrk {
+namespace hqc {
+
+constexpr int SEED = 40, SALT = 16, SSB = 64;
+
+template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_>
+struct Params {
+  static constexpr int N = N_, N1 = N1_, N2 = N2_, W = W_, WR = WR_, WE = WE_, K = K_, DELTA = DELTA_,
+                       MULT = MULT_, WPT = WPT_;
+  static constexpr int NB = (N + 7) / 8, VB = N1 * N2 / 8;
+  static constexpr int NW32 = (N + 31) / 32, VW32 = VB / 4, N32 = N >> 5, NR = N & 31;
+  static constexpr int NHW = (NB + 7) / 8;  // h stream words (the seedexpander squeezes 8-byte units)
+  static constexpr int PK = SEED + NB, SK = SEED + K + PK, CT = NB + VB + SALT, KPC = 2 * SEED + K, ENC = K + SALT;
+  static constexpr int RWW = (4 * W + 7) / 8, RWR = (4 * WR + 7) / 8, RWE = (4 * WE + 7) / 8;
+  static constexpr int NWP = 256 * WPT, NH2 = NWP + N32 + 2;
+  static constexpr int MSGB = K + NB + VB, MW = (MSGB + 2 + 7) / 8;  // K-hash message || 0x05 || 0x1F, words
+  static constexpr int MBW = ((SK > 8 * MW ? SK : 8 * MW) + 15) / 4;  // LDS byte buffer, words
+  static constexpr int T2 = 2 * DELTA, WMAX = W > WR ? W : WR;
+  static constexpr int ROW_KG = 2 * RWW + NHW, ROW_ENC = 2 * RWR + RWE + NHW;
+  static constexpr int ROWW = ROW_ENC > ROW_KG ? ROW_ENC : ROW_KG;
+  static_assert(NR != 0, "n is never a multiple of 32 for HQC");
+  static_assert(T2 + 1 <= 64 && WMAX <= 192 && N1 <= 128, "lane mappings");
+  static_assert(NWP >= NW32, "WPT too small");
+};
+template <int L> struct HQ;
+template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 3> {};
+template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 5> {};
+template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 8> {};
+
+// ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
+struct GfTabs {
+  uint8_t exp[512];
+  uint8_t log[256];
+};
+constexpr GfTabs make_gf() {
+  GfTabs t{};
+  unsigned x = 1;
+  for (int i = 0; i < 255; ++i) {
+    t.exp[i] = (uint8_t)x;
+    t.log[x] = (uint8_t)i;
+    x <<= 1;
+    if (x & 0x100) x ^= 0x11D;
+  }
+  for (int i = 255; i < 512; ++i) t.exp[i] = t.exp[i - 255];
+  return t;
+}
+constexpr GfTabs GFC = make_gf();
+__constant__ GfTabs GF = GFC;
+
+constexpr uint8_t cgmul(uint8_t a, uint8_t b) { return (a && b) ? GFC.exp[GFC.log[a] + GFC.log[b]] : 0; }
+
+// Reed-Solomon parity as a linear map: parity(m) = sum_i m_i PAR[i][.], rows = parity of unit messages
+// (the LFSR encoder of the spec is GF(2^8)-linear in m).  Stored as logarithms, 255 = zero.
+template <int L>
+struct RsTab {
+  uint8_t lp[HQ<L>::K][HQ<L>::T2];
+};
+template <int L>
+constexpr RsTab<L> make_rs() {
+  using P = HQ<L>;
+  uint8_t g[P::T2 + 1] = {};
+  g[0] = 1;
+  for (int i = 1; i <= P::T2; ++i) {  // g *= (x + alpha^i)
+    const uint8_t a = GFC.exp[i];
+    for (int j = i; j >= 1; --j) g[j] = (uint8_t)(g[j - 1] ^ cgmul(g[j], a));
+    g[0] = cgmul(g[0], a);
+  }
+  RsTab<L> t{};
+  for (int u = 0; u < P::K; ++u) {
+    uint8_t msg[P::K] = {};
+    msg[u] = 1;
+    uint8_t cdw[P::T2] = {};
+    for (int i = 0; i < P::K; ++i) {
+      const uint8_t gate = (uint8_t)(msg[P::K - 1 - i] ^ cdw[P::T2 - 1]);
+      for (int j = P::T2 - 1; j > 0; --j) cdw[j] = (uint8_t)(cdw[j - 1] ^ cgmul(gate, g[j]));
+      cdw[0] = cgmul(gate, g[0]);
+    }
+    for (int j = 0; j < P::T2; ++j) t.lp[u][j] = cdw[j] ? GFC.log[cdw[j]] : 255;
+  }
+  return t;
+}
+constexpr RsTab<128> RS128 = make_rs<128>();
+constexpr RsTab<192> RS192 = make_rs<192>();
+constexpr RsTab<256> RS256 = make_rs<256>();
+__constant__ RsTab<128> RSD128 = RS128;
+__constant__ RsTab<192> RSD192 = RS192;
+__constant__ RsTab<256> RSD256 = RS256;
+template <int L>
+__device__ __forceinline__ const RsTab<L>& rs_tab() {
+  if constexpr (L == 128) return RSD128;
+  else if constexpr (L == 192) return RSD192;
+  else return RSD256;
+}
+
+struct Lgf {
+  const uint8_t* e;  // exp[512] in LDS
+  const uint8_t* l;  // log[256] in LDS
+  __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b) const {
+    const uint32_t r = e[l[a] + l[b]];
+    return (a && b) ? r : 0u;
+  }
+  __device__ __forceinline__ uint32_t inv(uint32_t a) const { return e[255 - l[a]]; }
+};
+
+// ---------------------------------------------------------------- small helpers
+__device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+  return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+
+// little-endian 8 bytes at an arbitrary address: aligned dword loads, each holding at least
+// one byte of the field (so a load never leaves the page the field lies in)
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* b = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  const uint32_t w0 = b[0], w1 = b[1];
+  const uint32_t w2 = sh ? b[2] : 0u;
+  return (uint64_t)alignbit(w1, w0, sh) | ((uint64_t)alignbit(w2, w1, sh) << 32);
+}
+
+// one-block SHAKE256 over NWM words that already hold the message, domain byte and 0x1F pad
+template <int NWM>
+__device__ __forceinline__ void shake256_block(KState& s, const uint64_t (&w)[NWM]) {
+  static_assert(NWM <= RW_SHAKE256, "one block");
+  kzero(s);
+#pragma unroll
+  for (int i = 0; i < NWM; ++i) kxor(s, i, w[i]);
+  s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+}
+
+// seedexpander(seed) = SHAKE256(seed || 0x02)
+__device__ __forceinline__ void seedexp_init(KState& s, const uint64_t (&seed)[5]) {
+  uint64_t w[6] = {seed[0], seed[1], seed[2], seed[3], seed[4], 0x02ull | (0x1Full << 8)};
+  shake256_block<6>(s, w);
+}
+
+// squeeze NW words of a sponge into out[0..NW)
+__device__ __forceinline__ void squeeze_words(KState& s, uint64_t* out, int NW) {
+  int w = 0;
+#pragma unroll 1
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < RW_SHAKE256; ++i)
+      if (w + i < NW) out[w + i] = kword(s, i);
+    w += RW_SHAKE256;
+    if (w >= NW) break;
+    keccak_f(s);
+  }
+}
+
+// ---------------------------------------------------------------- lane / hs: seedexpander streams
+// row: [x words RWW][y words RWW][h words NHW]
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_kg_expand(const uint8_t* __restrict__ coins, size_t n,
+                                                       uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint8_t* c = coins + hs * P::KPC;
+  uint64_t* r = row + hs * P::ROWW;
+  uint64_t sd[5];
+  KState s;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sd[i] = ld64u(c + 8 * i);
+  seedexp_init(s, sd);
+  squeeze_words(s, r, 2 * P::RWW);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sd[i] = ld64u(c + SEED + P::K + 8 * i);
+  seedexp_init(s, sd);
+  squeeze_words(s, r + 2 * P::RWW, P::NHW);
+}
+
+// row: [r1 RWR][r2 RWR][e RWE][h NHW].  m, pk, salt at arbitrary byte addresses (Encaps:
+// coins / pk; Decaps re-encryption: m' / the pk inside sk / the salt inside ct).
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_enc_expand(const uint8_t* __restrict__ m, size_t m_stride,
+                                                        const uint8_t* __restrict__ pk, size_t pk_stride,
+                                                        const uint8_t* __restrict__ salt, size_t salt_stride,
+                                                        size_t n, uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  constexpr int KW = P::K / 8, TW = KW + 10 + 2 + 1;  // m || pk[0:80] || salt || (0x03, 0x1F)
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint8_t* mp = m + hs * m_stride;
+  const uint8_t* pp = pk + hs * pk_stride;
+  const uint8_t* sp = salt + hs * salt_stride;
+  uint64_t* r = row + hs * P::ROWW;
+  uint64_t w[TW];
+#pragma unroll
+  for (int i = 0; i < KW; ++i) w[i] = ld64u(mp + 8 * i);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) w[KW + i] = ld64u(pp + 8 * i);
+  w[KW + 10] = ld64u(sp);
+  w[KW + 11] = ld64u(sp + 8);
+  w[KW + 12] = 0x03ull | (0x1Full << 8);
+  KState s;
+  shake256_block<TW>(s, w);
+  uint64_t sd[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sd[i] = kword(s, i);  // theta[0:40]
+  seedexp_init(s, sd);
+  squeeze_words(s, r, 2 * P::RWR + P::RWE);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sd[i] = ld64u(pp + 8 * i);
+  seedexp_init(s, sd);
+  squeeze_words(s, r + 2 * P::RWR + P::RWE, P::NHW);
+}
+
+// row: [x words RWW][y words RWW]
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_dec_expand(const uint8_t* __restrict__ sk, size_t n,
+                                                        uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint8_t* k = sk + hs * P::SK;
+  uint64_t sd[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sd[i] = ld64u(k + 8 * i);
+  KState s;
+  seedexp_init(s, sd);
+  squeeze_words(s, row + hs * P::ROWW, 2 * P::RWW);
+}
+
+// ss = SHAKE256(msg) over MW padded words per hs (msg || 0x05 || 0x1F || 0*)
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_hash(const uint64_t* __restrict__ msg, size_t n, uint8_t* __restrict__ ss) {
+  using P = HQ<L>;
+  constexpr int RW = RW_SHAKE256, NFULL = (P::MW - 1) / RW, REM = P::MW - NFULL * RW;
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  const uint64_t* m = msg + hs * P::MW;
+  KState s;
+  kzero(s);
+  uint64_t nxt[RW];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) nxt[i] = (NFULL > 0 || i < REM) ? m[i] : 0;
+#pragma unroll 1
+  for (int b = 0; b < NFULL; ++b) {
+#pragma unroll
+    for (int i = 0; i < RW; ++i) kxor(s, i, nxt[i]);
+    const int nb = (b + 1) * RW;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) nxt[i] = (b + 1 < NFULL || i < REM) ? m[nb + i] : 0;
+    keccak_f(s);
+  }
+#pragma unroll
+  for (int i = 0; i < REM; ++i) kxor(s, i, nxt[i]);
+  s.a[RW - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  uint64_t* o = (uint64_t*)(ss + hs * SSB);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = kword(s, i);
+}
+
+// ---------------------------------------------------------------- workgroup / hs helpers
+// support of a fixed-weight vector from its random words: s_i = i + floor(r_i (n - i) / 2^32)
+template <int L>
+__device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, uint32_t* sup) {
+  using P = HQ<L>;
+  const uint32_t* r32 = (const uint32_t*)words;
+  for (int i = threadIdx.x; i < weight; i += 256)
+    sup[i] = (uint32_t)i + __umulhi(r32[i], (uint32_t)(P::N - i));
+}
+
+// one wave: for i = weight-2 .. 0, s_i := i when s_i equals some s_j with j > i (branch-free;
+// lanes hold j = lane, lane + 64, lane + 128)
+__device__ __forceinline__ void dedupe_wave(uint32_t* sup, int weight) {
+  const int lane = threadIdx.x & 63;
+  uint32_t f[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) f[q] = (lane + 64 * q < weight) ? sup[lane + 64 * q] : 0xFFFFFFFFu;
+#pragma unroll 1
+  for (int i = weight - 2; i >= 0; --i) {
+    const int qi = i >> 6, li = i & 63;
+    const uint32_t oi = __builtin_amdgcn_readlane(qi == 0 ? f[0] : (qi == 1 ? f[1] : f[2]), li);
+    bool hit = false;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) hit |= (lane + 64 * q > i) && (f[q] == oi);
+    const bool found = __ballot(hit) != 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (found && lane + 64 * q == i) f[q] = (uint32_t)i;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (lane + 64 * q < weight) sup[lane + 64 * q] = f[q];
+}
+
+// doubled dense operand: D[q] = raw[q] ^ (clean << n)[q], raw words via rd(j) (0 outside [0, NW32)),
+// clean = raw masked to n bits.  Written for q in [0, NH2).
+template <int L, typename Rd>
+__device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
+  using P = HQ<L>;
+  constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
+  auto clean = [&](int j) -> uint32_t {
+    if (j < 0 || j >= P::NW32) return 0u;
+    const uint32_t v = rd(j);
+    return j == P::NW32 - 1 ? (v & TOPMASK) : v;
+  };
+  for (int q = threadIdx.x; q < P::NH2; q += 256) {
+    uint32_t v = q < P::NW32 ? rd(q) : 0u;
+    if (q >= P::N32) v ^= alignbit(clean(q - P::N32), clean(q - P::N32 - 1), 32 - P::NR);
+    D[q] = v;
+  }
+}
+
+// acc[c] ^= word (j0 + c) of X^k D-operand, for every position k of sup
+template <int L, int NV>
+__device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, const uint32_t* const (&D)[NV],
+                                             uint32_t (&acc)[NV][HQ<L>::WPT]) {
+  using P = HQ<L>;
+  const int j0 = threadIdx.x * P::WPT;
+#pragma unroll 1
+  for (int i = 0; i < weight; ++i) {
+    const uint32_t k = sup[i];
+    const uint32_t e = (uint32_t)P::N - k;
+    const int off = (int)(e >> 5) + j0;
+    const uint32_t sh = e & 31;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      uint32_t w[P::WPT + 1];
+#pragma unroll
+      for (int c = 0; c <= P::WPT; ++c) w[c] = D[v][off + c];
+#pragma unroll
+      for (int c = 0; c < P::WPT; ++c) acc[v][c] ^= alignbit(w[c + 1], w[c], sh);
+    }
+  }
+}
+
+// RM(1,7) codeword word q (0..3) of symbol b: bit j = b7 ^ <b0..6, j>
+__device__ __forceinline__ uint32_t rm_word(uint32_t b, int q) {
+  uint32_t w = 0u - (b >> 7 & 1);
+  w ^= (0u - (b & 1)) & 0xaaaaaaaau;
+  w ^= (0u - (b >> 1 & 1)) & 0xccccccccu;
+  w ^= (0u - (b >> 2 & 1)) & 0xf0f0f0f0u;
+  w ^= (0u - (b >> 3 & 1)) & 0xff00ff00u;
+  w ^= (0u - (b >> 4 & 1)) & 0xffff0000u;
+  w ^= (0u - (b >> 5 & 1)) & (0u - (uint32_t)(q & 1));
+  w ^= (0u - (b >> 6 & 1)) & (0u - (uint32_t)(q >> 1 & 1));
+  return w;
+}
+
+__device__ __forceinline__ uint32_t lds_u32_unaligned(const uint8_t* b, int off) {
+  return (uint32_t)b[off] | (uint32_t)b[off + 1] << 8 | (uint32_t)b[off + 2] << 16 | (uint32_t)b[off + 3] << 24;
+}
+__device__ __forceinline__ void lds_store_u32_unaligned(uint8_t* b, int off, uint32_t v) {
+  b[off] = (uint8_t)v;
+  b[off + 1] = (uint8_t)(v >> 8);
+  b[off + 2] = (uint8_t)(v >> 16);
+  b[off + 3] = (uint8_t)(v >> 24);
+}
+
+__device__ __forceinline__ void fill_gf(uint8_t* e, uint8_t* l) {
+  for (int i = threadIdx.x; i < 512; i += 256) e[i] = GF.exp[i];
+  for (int i = threadIdx.x; i < 256; i += 256) l[i] = GF.log[i];
+}
+
+// ---------------------------------------------------------------- KeyGen: s = x + y h
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
+                                                    const uint8_t* __restrict__ coins, uint8_t* __restrict__ pk,
+                                                    uint8_t* __restrict__ sk) {
+  using P = HQ<L>;
+  __shared__ uint32_t D[P::NH2];
+  __shared__ uint32_t MB[P::MBW];
+  __shared__ uint32_t SX[P::WMAX], SY[P::WMAX];
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const int t = threadIdx.x, wave = t >> 6;
+  const uint64_t* rw = row + hs * P::ROWW;
+  const uint8_t* c = coins + hs * P::KPC;
+  uint8_t* mb = (uint8_t*)MB;
+  const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWW);
+  build_doubled<L>(D, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });  // h: n bits
+  supports_raw<L>(rw, P::W, SX);
+  supports_raw<L>(rw + P::RWW, P::W, SY);
+  // sk = sk_seed || sigma || pk_seed || s  (the coins' first 80 + K bytes, in order)
+  for (int b = t; b < P::KPC; b += 256) mb[b] = c[b];
+  __syncthreads();
+  if (wave == 0) dedupe_wave(SX, P::W);
+  if (wave == 1) dedupe_wave(SY, P::W);
+  __syncthreads();
+  uint32_t acc[1][P::WPT] = {};
+  const uint32_t* const Ds[1] = {D};
+  sparse_dense<L, 1>(SY, P::W, Ds, acc);
+  __syncthreads();  // D is reused as the output buffer
+  const int j0 = t * P::WPT;
+#pragma unroll
+  for (int q = 0; q < P::WPT; ++q) D[j0 + q] = acc[0][q];
+  __syncthreads();
+  for (int i = t; i < P::W; i += 256) atomicXor(&D[SX[i] >> 5], 1u << (SX[i] & 31));
+  __syncthreads();
+  constexpr int SOFF = (2 * SEED + P::K) / 4;  // s at byte 80 + K (a multiple of 4)
+  for (int j = t; j < P::NW32; j += 256) MB[SOFF + j] = j == P::NW32 - 1 ? (D[j] & ((1u << P::NR) - 1)) : D[j];
+  __syncthreads();
+  uint8_t* so = sk + hs * P::SK;
+  uint8_t* po = pk + hs * P::PK;
+  for (int b = t; b < P::SK; b += 256) so[b] = mb[b];
+  for (int b = t; b < P::PK; b += 256) po[b] = mb[SEED + P::K + b];
+}
+
+// ---------------------------------------------------------------- Encaps / re-encryption
+// Encaps (REENC = false): m, salt from coins; s from pk; writes ct and the K-hash message rows.
+// Decaps re-encryption (REENC = true): m' from mp; s and sigma from sk; compares (u', v') with the
+// received ct; message = (m' if equal else sigma) || u || v of the received ct; status -1 if unequal.
+template <int L, bool REENC>
+__global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
+                                                     const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
+                                                     uint8_t* __restrict__ ct_out, const uint8_t* __restrict__ mp,
+                                                     const uint8_t* __restrict__ sk, const uint8_t* __restrict__ ct_in,
+                                                     int32_t* __restrict__ status, uint64_t* __restrict__ msg) {
+  using P = HQ<L>;
+  __shared__ uint32_t D1[P::NH2], D2[P::NH2];
+  __shared__ __attribute__((aligned(16))) uint32_t MB[P::MBW];
+  __shared__ uint32_t S1[P::WMAX], S2[P::WMAX], SE[P::WMAX];
+  __shared__ uint8_t GE[512], GL[256], SYM[128], MM[32];
+  __shared__ uint32_t DIFF;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const uint64_t* rw = row + hs * P::ROWW;
+  uint8_t* mb = (uint8_t*)MB;
+  const uint8_t* spk = REENC ? sk + hs * P::SK + SEED + P::K : pk + hs * P::PK;  // the pk
+  // phase A: h doubled, s staged (bytes), supports, m, GF tables
+  const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
+  build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });
+  for (int b = t; b < 4 * P::NW32; b += 256) mb[b] = b < P::NB ? spk[SEED + b] : 0;
+  supports_raw<L>(rw, P::WR, S1);
+  supports_raw<L>(rw + P::RWR, P::WR, S2);
+  supports_raw<L>(rw + 2 * P::RWR, P::WE, SE);
+  fill_gf(GE, GL);
+  if (t < P::K) MM[t] = REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t];
+  if (t == 0) DIFF = 0;
+  __syncthreads();
+  // phase B: s doubled (keeps stray bits of a malformed pk), dedupe, RS parity
+  build_doubled<L>(D2, [&](int j) { return MB[j]; });
+  if (wave == 0) dedupe_wave(S1, P::WR);
+  if (wave == 1) dedupe_wave(S2, P::WR);
+  if (wave == 2) dedupe_wave(SE, P::WE);
+  if (wave == 3) {
+    const RsTab<L>& rs = rs_tab<L>();
+    if (lane < P::T2) {
+      uint32_t par = 0;
+      for (int i = 0; i < P::K; ++i) {
+        const uint32_t mi = MM[i], lp = rs.lp[i][lane];
+        const uint32_t pr = GE[GL[mi] + lp];
+        par ^= (mi != 0 && lp != 255) ? pr : 0u;
+      }
+      SYM[lane] = (uint8_t)par;
+    } else if (lane < P::T2 + P::K) {
+      SYM[lane] = MM[lane - P::T2];
+    }
+    if (lane + 64 < P::N1) SYM[lane + 64] = MM[lane + 64 - P::T2];
+  }
+  __syncthreads();
+  // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
+  uint32_t acc[2][P::WPT] = {};
+  const uint32_t* const Ds[2] = {D1, D2};
+  sparse_dense<L, 2>(S2, P::WR, Ds, acc);
+  __syncthreads();
+  const int j0 = t * P::WPT;
+#pragma unroll
+  for (int q = 0; q < P::WPT; ++q) D1[j0 + q] = acc[0][q], D2[j0 + q] = acc[1][q];
+  __syncthreads();
+  for (int i = t; i < P::WR; i += 256) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
+  for (int i = t; i < P::WE; i += 256) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
+  __syncthreads();
+  constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
+  constexpr int UOFF = P::K / 4;  // u at message byte K
+  auto vword = [&](int j) {       // v word j = (r2 s + e + codeword) word j
+    const int sym = j / (4 * P::MULT);
+    return D2[j] ^ rm_word(SYM[sym], j & 3);
+  };
+  if constexpr (!REENC) {
+    for (int j = t; j < P::NW32; j += 256) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
+    if (t < P::K) mb[t] = MM[t];
+    __syncthreads();  // the last u word's spare bytes are v's first bytes
+    for (int j = t; j < P::VW32; j += 256) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
+  } else {
+    // received u || v into the message area, then compare with the re-encryption
+    const uint8_t* cin = ct_in + hs * P::CT;
+    for (int b = t; b < P::NB + P::VB; b += 256) mb[P::K + b] = cin[b];
+    __syncthreads();
+    uint32_t diff = 0;
+    for (int j = t; j < P::NW32; j += 256) {
+      uint32_t u = D1[j], c = MB[UOFF + j];
+      if (j == P::NW32 - 1) {
+        u &= TOPMASK;
+        constexpr int VALID = P::NB - 4 * (P::NW32 - 1);  // bytes of the last word that belong to u
+        constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+        c &= BM;
+      }
+      diff |= u ^ c;
+    }
+    for (int j = t; j < P::VW32; j += 256) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
+    if (diff) atomicOr(&DIFF, 1u);
+    __syncthreads();
+    const bool ok = DIFF == 0;
+    if (t < P::K) mb[t] = ok ? MM[t] : sk[hs * P::SK + SEED + t];
+    if (t == 0) status[hs] = ok ? 0 : -1;
+  }
+  for (int b = P::MSGB + t; b < 8 * P::MW; b += 256) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
+  __syncthreads();
+  // phase E: K-hash message rows (aligned words), ciphertext bytes
+  const uint64_t* m64 = (const uint64_t*)MB;
+  uint64_t* mo = msg + hs * P::MW;
+  for (int w = t; w < P::MW; w += 256) mo[w] = m64[w];
+  if constexpr (!REENC) {
+    uint8_t* co = ct_out + hs * P::CT;
+    for (int b = t; b < P::NB + P::VB; b += 256) co[b] = mb[P::K + b];
+    if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
+  }
+}
+
+// ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
+                                                    const uint8_t* __restrict__ ct, uint8_t* __restrict__ mp) {
+  using P = HQ<L>;
+  __shared__ uint32_t D1[P::NH2];
+  __shared__ uint32_t T[P::NWP];
+  __shared__ uint32_t MB[(P::NB + P::VB + 8) / 4 + 1];
+  __shared__ uint32_t SY[P::WMAX];
+  __shared__ uint8_t GE[512], GL[256], SYM[128], SYN[64], CL[64], OM[64];
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const uint64_t* rw = row + hs * P::ROWW;
+  uint8_t* mb = (uint8_t*)MB;
+  const uint8_t* c = ct + hs * P::CT;
+  for (int b = t; b < 4 * P::NW32; b += 256) mb[b] = b < P::NB + P::VB ? c[b] : 0;
+  for (int b = 4 * P::NW32 + t; b < P::NB + P::VB; b += 256) mb[b] = c[b];
+  supports_raw<L>(rw + P::RWW, P::W, SY);
+  fill_gf(GE, GL);
+  __syncthreads();
+  // u doubled: raw words = the ct's u bytes (bits >= n as received); the word straddling into v is cut
+  constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
+  constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+  build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? (MB[j] & BM) : MB[j]; });
+  if (wave == 0) dedupe_wave(SY, P::W);
+  __syncthreads();
+  uint32_t acc[1][P::WPT] = {};
+  const uint32_t* const Ds[1] = {D1};
+  sparse_dense<L, 1>(SY, P::W, Ds, acc);
+  const int j0 = t * P::WPT;
+#pragma unroll
+  for (int q = 0; q < P::WPT; ++q) {
+    const int j = j0 + q;
+    T[j] = j < P::VW32 ? acc[0][q] ^ lds_u32_unaligned(mb, P::NB + 4 * j) : 0u;
+  }
+  __syncthreads();
+  // duplicated RM(1,7): one wave per symbol, lane l holds positions l and l + 64
+  for (int sym = wave; sym < P::N1; sym += 4) {
+    const uint32_t* cw = T + sym * 4 * P::MULT;
+    int x0 = 0, x1 = 0;
+#pragma unroll
+    for (int cp = 0; cp < P::MULT; ++cp) {
+      x0 += (int)(cw[4 * cp + (lane >> 5)] >> (lane & 31) & 1);
+      x1 += (int)(cw[4 * cp + 2 + (lane >> 5)] >> (lane & 31) & 1);
+    }
+    {
+      const int a = x0, b = x1;
+      x0 = a + b;
+      x1 = a - b;
+    }
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+      const int p0 = __shfl_xor(x0, 1 << bit), p1 = __shfl_xor(x1, 1 << bit);
+      const bool hi = (lane >> bit) & 1;
+      x0 = hi ? p0 - x0 : x0 + p0;
+      x1 = hi ? p1 - x1 : x1 + p1;
+    }
+    if (lane == 0) x0 -= 64 * P::MULT;
+    // first maximum of |value| (lowest index), sign -> bit 7
+    const uint32_t k0 = ((uint32_t)abs(x0) << 8) | ((uint32_t)(127 - lane) << 1) | (x0 > 0 ? 1u : 0u);
+    const uint32_t k1 = ((uint32_t)abs(x1) << 8) | ((uint32_t)(63 - lane) << 1) | (x1 > 0 ? 1u : 0u);
+    uint32_t k = k0 > k1 ? k0 : k1;
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) {
+      const uint32_t o = __shfl_xor(k, 1 << bit);
+      k = o > k ? o : k;
+    }
+    if (lane == 0) SYM[sym] = (uint8_t)((127 - ((k >> 1) & 127)) | ((k & 1) << 7));
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // Reed-Solomon, bounded distance: syndromes S_{i+1} = r(alpha^(i+1)), i < 2 delta
+  const Lgf gf{GE, GL};
+  if (lane < P::T2) {
+    uint32_t s = 0, e = 0;
+    const uint32_t step = (uint32_t)(lane + 1);
+    for (int j = 0; j < P::N1; ++j) {
+      const uint32_t r = SYM[j];
+      const uint32_t pr = GE[GL[r] + e];
+      s ^= r ? pr : 0u;
+      e += step;
+      e = e >= 255 ? e - 255 : e;
+    }
+    SYN[lane] = (uint8_t)s;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // Berlekamp-Massey, lane j holds C_j, B_j (branch-free in the data)
+  uint32_t Cj = lane == 0 ? 1u : 0u, Bj = Cj, b = 1;
+  int Lr = 0, m = 1;
+  for (int i = 0; i < P::T2; ++i) {
+    const uint32_t term = (lane <= Lr && lane <= i) ? gf.mul(Cj, SYN[i - (lane <= i ? lane : 0)]) : 0u;
+    uint32_t d = term;
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit) d ^= __shfl_xor(d, 1 << bit);
+    const uint32_t coef = gf.mul(d, gf.inv(b));
+    const uint32_t bsh = __shfl(Bj, lane - m >= 0 ? lane - m : 0);
+    const uint32_t cn = Cj ^ (lane >= m ? gf.mul(coef, bsh) : 0u);
+    const bool upd = d != 0 && 2 * Lr <= i;
+    Bj = upd ? Cj : Bj;
+    b = upd ? d : b;
+    Lr = upd ? i + 1 - Lr : Lr;
+    m = upd ? 1 : m + 1;
+    Cj = cn;
+  }
+  if (lane <= P::T2) CL[lane] = (uint8_t)Cj;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // Omega = S(x) C(x) mod x^(2 delta)
+  if (lane < P::T2) {
+    uint32_t o = 0;
+    for (int j = 0; j <= lane; ++j) o ^= gf.mul(SYN[lane - j], CL[j]);
+    OM[lane] = (uint8_t)o;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // Chien search + Forney over the n1 positions
+  for (int pos = lane; pos < P::N1; pos += 64) {
+    const uint32_t lx = (uint32_t)((255 - pos) % 255);  // log of alpha^(-pos)
+    auto mulx = [&](uint32_t a) { return a ? (uint32_t)GE[GL[a] + lx] : 0u; };
+    uint32_t cv = 0, dv = 0, ov = 0;
+    for (int i = P::T2; i >= 0; --i) cv = mulx(cv) ^ CL[i];
+    for (int i = P::T2 - 1; i >= 0; --i) {
+      dv = mulx(dv) ^ ((i & 1) == 0 ? CL[i + 1] : 0u);
+      ov = mulx(ov) ^ OM[i];
+    }
+    const uint32_t fix = (cv == 0 && dv != 0) ? gf.mul(ov, gf.inv(dv)) : 0u;
+    SYM[pos] ^= (uint8_t)fix;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < P::K) mp[hs * 32 + lane] = SYM[P::T2 + lane];
+}
+
+// ---------------------------------------------------------------- launchers
+inline unsigned blocks_for(size_t t) { return (unsigned)((t + 255) / 256); }
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <int L>
+size_t scratch_t(size_t C) {
+  using P = HQ<L>;
+  return al256(C * P::ROWW * 8) + al256(C * P::MW * 8) + al256(C * 32) + al256(C * 4);
+}
+struct View {
+  uint64_t* row;
+  uint64_t* msg;
+  uint8_t* mp;
+  int32_t* st;
+};
+template <int L>
+View carve(void* base, size_t C) {
+  using P = HQ<L>;
+  uint8_t* p = (uint8_t*)base;
+  View v;
+  v.row = (uint64_t*)p;
+  p += al256(C * P::ROWW * 8);
+  v.msg = (uint64_t*)p;
+  p += al256(C * P::MW * 8);
+  v.mp = p;
+  p += al256(C * 32);
+  v.st = (int32_t*)p;
+  return v;
+}
+
+template <int L>
+hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
+  View v = carve<L>(scratch, n);
+  QRK_LAUNCH("k_hqc_kg_expand", st, k_hqc_kg_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, v.row);
+  QRK_LAUNCH("k_hqc_kg_mul", st, k_hqc_kg_mul<L>, dim3((unsigned)n), dim3(256), 0, st, n, v.row, coins, pk, sk);
+  return hipGetLastError();
+}
+
+template <int L>
+hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins, void* scratch,
+                    hipStream_t st) {
+  using P = HQ<L>;
+  View v = carve<L>(scratch, n);
+  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins,
+             (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, v.row);
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(256), 0, st, n, v.row, coins,
+             pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
+             v.msg);
+  QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
+  return hipGetLastError();
+}
+
+template <int L>
+hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, int32_t* status, void* scratch,
+                    hipStream_t st) {
+  using P = HQ<L>;
+  View v = carve<L>(scratch, n);
+  int32_t* stp = status ? status : v.st;
+  QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.row);
+  QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(256), 0, st, n, v.row, ct, v.mp);
+  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.mp, (size_t)32,
+             sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row);
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(256), 0, st, n, v.row,
+             (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
+  QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
+  return hipGetLastError();
+}
+
+}  // namespace hqc
+
+size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk) {
+  switch (a.k) {
+    case 128: return hqc::scratch_t<128>(chunk);
+    case 192: return hqc::scratch_t<192>(chunk);
+    default: return hqc::scratch_t<256>(chunk);
+  }
+}
+
+hipError_t hqc_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
+                       const Streams& s) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 128: return hqc::keypair_t<128>(n, pk, sk, coins, scratch, s.main);
+    case 192: return hqc::keypair_t<192>(n, pk, sk, coins, scratch, s.main);
+    case 256: return hqc::keypair_t<256>(n, pk, sk, coins, scratch, s.main);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t hqc_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
+                      void* scratch, const Streams& s) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 128: return hqc::encaps_t<128>(n, ct, ss, pk, coins, scratch, s.main);
+    case 192: return hqc::encaps_t<192>(n, ct, ss, pk, coins, scratch, s.main);
+    case 256: return hqc::encaps_t<256>(n, ct, ss, pk, coins, scratch, s.main);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t hqc_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, int32_t* status,
+                      void* scratch, const Streams& s) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 128: return hqc::decaps_t<128>(n, ss, ct, sk, status, scratch, s.main);
+    case 192: return hqc::decaps_t<192>(n, ss, ct, sk, status, scratch, s.main);
+    case 256: return hqc::decaps_t<256>(n, ss, ct, sk, status, scratch, s.main);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace qrk

@@ -7,13 +7,13 @@
 
 namespace qrk {
 
-enum class Family { MLKEM, FRODO };
+enum class Family { MLKEM, FRODO, HQC };
 
 struct AlgInfo {
   const char* name;
   Family family;
   int level;        // claimed NIST level (OQS_KEM.claimed_nist_level)
-  int k;            // ML-KEM module rank, or Frodo n
+  int k;            // ML-KEM module rank, Frodo n, or HQC security bits (128/192/256)
   size_t pk, sk, ct, ss;
   size_t kp_coins, enc_coins;  // bytes drawn by one keypair / encaps randombytes call
   bool aes;         // Frodo A generated with AES-128 (else SHAKE128)
@@ -50,6 +50,7 @@ struct Scratch {
 // Per-chunk scratch requirement (bytes) for `chunk` handshakes of `a`.
 size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk);
 size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk);
+size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 
 // Main stream (the caller's) plus an optional side stream and two events used
 // to fork/join independent kernel chains inside one operation.
@@ -74,6 +75,15 @@ hipError_t frodo_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, co
                         const uint8_t* coins, void* scratch, const Streams& st);
 hipError_t frodo_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
                         void* scratch, const Streams& st);
+
+// HQC: decaps writes status[i] = -1 when the re-encryption check fails (ss = K(sigma || ct) is
+// still written), the OQS_KEM_decaps return of liboqs; status may be NULL.
+hipError_t hqc_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
+                       const Streams& st);
+hipError_t hqc_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
+                      void* scratch, const Streams& st);
+hipError_t hqc_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, int32_t* status,
+                      void* scratch, const Streams& st);
 
 // SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len) for i < n, len <= 136.
 hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st);

@@ -144,11 +144,18 @@ class BatchKEM:
         return (c, ss, st) if return_status else (c, ss)
 
     # ------------------------------------------------------------------ Decaps
-    def decaps(self, sk, ct_):
-        """Returns ss [n, ss_len]; implicit rejection (never fails on well-sized input)."""
+    def decaps(self, sk, ct_, return_status: bool = False):
+        """Returns ss [n, ss_len] (+ status int32[n] with return_status).  ML-KEM / FrodoKEM:
+        implicit rejection, status 0.  HQC: status -1 where the re-encryption check fails (the
+        OQS_ERROR liboqs returns there); ss = K(sigma || ct) is written either way."""
         if _is_dev(sk) and _is_dev(ct_):
             n = sk.shape[0]
             ss = self._empty(n, self.ss_len)
+            if return_status:
+                st = torch.empty((n,), dtype=torch.int32, device=sk.device)
+                self._check(LIB.qrk_kem_decaps_batch_status(self._ctx, self._name, n, _dptr(ss), _dptr(ct_),
+                                                            _dptr(sk), _dptr(st), self._stream()), "decaps")
+                return ss, st
             self._check(LIB.qrk_kem_decaps_batch(self._ctx, self._name, n, _dptr(ss), _dptr(ct_), _dptr(sk),
                                                  self._stream()), "decaps")
             return ss
@@ -157,9 +164,10 @@ class BatchKEM:
         if s.shape[0] != c.shape[0]:
             raise ValueError("sk and ct batch sizes differ")
         ss = np.zeros((s.shape[0], self.ss_len), np.uint8)
-        self._check(LIB.qrk_kem_decaps_batch_host(self._ctx, self._name, s.shape[0], _hptr(ss), _hptr(c), _hptr(s)),
-                    "decaps")
-        return ss
+        st = np.zeros((s.shape[0],), np.int32)
+        self._check(LIB.qrk_kem_decaps_batch_status_host(self._ctx, self._name, s.shape[0], _hptr(ss), _hptr(c),
+                                                         _hptr(s), _hptr(st)), "decaps")
+        return (ss, st) if return_status else ss
 
     @property
     def effective_chunk(self) -> int:

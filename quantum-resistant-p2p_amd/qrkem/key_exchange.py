@@ -12,9 +12,10 @@ Drop-in counterpart of ``quantum_resistant_p2p/crypto/key_exchange.py``:
 * ``FrodoKEMKeyExchange(security_level=3, use_aes=True)`` -- AES/SHAKE variant
   maps and cross-PRG fallback (``:312-367``), keeping the reference's naming
   quirk: ``name`` reports the *requested* PRG even after a fallback (``:369-379``);
-* ``HQCKeyExchange`` -- same constructor contract (``:189-229``); HQC has no
-  kernel in this engine, so construction raises the reference's
-  ``ValueError("No HQC variant found ...")``.
+* ``HQCKeyExchange(security_level=3)`` -- levels 1/3/5 -> HQC-128/192/256, names
+  "HQC (Level n)", same constructor contract (``:189-229``).  As with liboqs, ``decapsulate``
+  raises ``RuntimeError`` when the ciphertext fails HQC's re-encryption check (liboqs's
+  HQC decaps returns an error there, surfaced by ``oqs.py:372-380``).
 
 Single-handshake methods keep the reference's call pattern (a fresh mechanism
 object for encaps/decaps) but every KEM operation runs on the GPU.  Added:

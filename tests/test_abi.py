@@ -62,17 +62,34 @@ def test_registry_and_errors():
     en = oqs.get_enabled_kem_mechanisms()
     assert {"ML-KEM-512", "ML-KEM-768", "ML-KEM-1024"} <= set(en)
     assert set(en) <= set(sup)
-    assert "HQC-128" in sup and "HQC-128" not in en
+    # every KEM the reference selects (key_exchange.py:75-79, 206-210, 332-343) is enabled
+    assert {"HQC-128", "HQC-192", "HQC-256"} <= set(en)
     assert not any(n.startswith("Kyber") for n in sup)  # different bytes from ML-KEM
     with pytest.raises(oqs.MechanismNotSupportedError):
         oqs.KeyEncapsulation("NoSuchKEM")
-    with pytest.raises(oqs.MechanismNotEnabledError):
-        oqs.KeyEncapsulation("HQC-128")
+    with pytest.raises(oqs.MechanismNotSupportedError):
+        oqs.KeyEncapsulation("BIKE-L1")
     assert oqs.oqs_version()
     from qrkem._native import LIB
     assert not LIB.OQS_KEM_new(b"NoSuchKEM")
     assert LIB.OQS_KEM_alg_is_enabled(b"ML-KEM-768") == 1
-    assert LIB.OQS_KEM_alg_is_enabled(b"HQC-256") == 0
+    assert LIB.OQS_KEM_alg_is_enabled(b"HQC-256") == 1
+
+
+# liboqs 0.12 sizes of the 2023-04-30 HQC (pk, sk, ct, ss) and our coin lengths
+HQC_SIZES = {"HQC-128": (2249, 2305, 4433, 64, 96, 32), "HQC-192": (4522, 4586, 8978, 64, 104, 40),
+             "HQC-256": (7245, 7317, 14421, 64, 112, 48)}
+
+
+@pytest.mark.parametrize("alg", sorted(HQC_SIZES))
+def test_hqc_sizes(alg):
+    from qrkem._native import LIB
+    out = (ct.c_size_t * 6)()
+    assert LIB.qrk_kem_sizes(alg.encode(), out) == 0
+    assert tuple(out) == HQC_SIZES[alg]
+    p = LIB.OQS_KEM_new(alg.encode())
+    assert p
+    LIB.OQS_KEM_free(p)
 
 
 def test_mem_cleanse():

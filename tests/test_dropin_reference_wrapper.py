@@ -48,8 +48,11 @@ def test_reference_wrapper_loads_qrkem(ref_oqs):
     assert k.details["length_ciphertext"] == 1088
     assert k.details["length_shared_secret"] == 32
     assert k.details["claimed_nist_level"] == 3 and k.details["is_ind_cca"]
-    with pytest.raises(ref_oqs.MechanismNotEnabledError):
-        ref_oqs.KeyEncapsulation("HQC-128")
+    h = ref_oqs.KeyEncapsulation("HQC-128")
+    assert (h.details["length_public_key"], h.details["length_secret_key"], h.details["length_ciphertext"],
+            h.details["length_shared_secret"]) == (2249, 2305, 4433, 64)
+    with pytest.raises(ref_oqs.MechanismNotSupportedError):
+        ref_oqs.KeyEncapsulation("BIKE-L1")
     with pytest.raises(ref_oqs.MechanismNotSupportedError):
         ref_oqs.KeyEncapsulation("Kyber768")
 

@@ -46,8 +46,8 @@ def test_bad_arguments_fail_loudly():
     assert LIB.qrk_ctx_create(ct.byref(h), 0) == 0
     assert LIB.qrk_kem_keypair_batch(h, b"Kyber768", 1, None, None, None, None) == -1
     assert "unsupported" in last_error()
-    assert LIB.qrk_kem_keypair_batch(h, b"HQC-128", 1, None, None, None, None) == -1
-    assert "not enabled" in last_error()
+    assert LIB.qrk_kem_keypair_batch(h, b"BIKE-L1", 1, None, None, None, None) == -1
+    assert "unsupported" in last_error()
     LIB.qrk_ctx_destroy(h)
 
 
