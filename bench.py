@@ -65,6 +65,9 @@ def valu_ops(alg, mode="encdec") -> int:
     """W = P*4320 + (NTT + NTT^-1)*896*8 + basemul_polys*3584 per Encaps+Decaps
     (mode "encdec") or per Decaps (mode "decaps-tampered").  FrodoKEM: P*4320 (the S'A
     contraction runs on MFMA and is priced separately)."""
+    if alg in HQ:
+        names = ["k_hqc_enc_expand", "k_hqc_enc_mul", "k_hqc_hash", "k_hqc_dec_expand", "k_hqc_decode"]
+        return sum(kernel_ops_per_hs(alg, nm, mode)[0] for nm in names)
     if alg in FP:
         p = frodo_perms(alg)
         enc = p["k_fr_front_enc"] + p["k_fr_gen_at"] + p["k_fr_se_stream"] + p["k_fr_ss"]
@@ -111,10 +114,42 @@ def frodo_perms(alg):
             "k_fr_front_enc": -(-(pk + 1) // rate) + 1, "k_fr_g2_dec": 1}
 
 
+# HQC (n, n1, n2, w, w_r, w_e, k): the 2023-04-30 HQC parameter sets (oracle/py/hqc_spec.py)
+HQ = {"HQC-128": (17669, 46, 384, 66, 75, 75, 16), "HQC-192": (35851, 56, 640, 100, 114, 114, 24),
+      "HQC-256": (57637, 90, 640, 131, 149, 149, 32)}
+# sparse-dense product in F2[X]/(X^n-1): one funnel shift + one XOR per (position, 32-bit word)
+SPARSE_OPS = 2
+
+
+def hqc_work(alg):
+    """Per-call algorithmic work of each HQC kernel: Keccak permutations (FIPS-minimal sponge
+    counts, 17-word SHAKE256 blocks) or sparse-dense word operations."""
+    n, n1, n2, w, wr, we, k = HQ[alg]
+    nb, vb = (n + 7) // 8, n1 * n2 // 8
+    nw32, vw32 = (n + 31) // 32, vb // 4
+    rw = lambda x: (4 * x + 7) // 8  # noqa: E731  seedexpander words of a weight-x vector
+    blocks = lambda words: -(-words // 17)  # noqa: E731
+    mw = (k + nb + vb + 2 + 7) // 8
+    return {"perms": {"k_hqc_enc_expand": 1 + blocks(2 * rw(wr) + rw(we)) + blocks((nb + 7) // 8),
+                      "k_hqc_dec_expand": blocks(2 * rw(w)), "k_hqc_hash": blocks(mw),
+                      "k_hqc_kg_expand": blocks(2 * rw(w)) + blocks((nb + 7) // 8)},
+            "ops": {"k_hqc_enc_mul": 2 * wr * nw32 * SPARSE_OPS, "k_hqc_decode": w * vw32 * SPARSE_OPS,
+                    "k_hqc_kg_mul": w * nw32 * SPARSE_OPS}}
+
+
 def kernel_ops_per_hs(alg, name, mode):
     """Algorithmic ops one handshake contributes to kernel `name` in one bench step
     (encaps+decaps, or decaps only) and the bound they are priced against."""
     calls = 2 if mode == "encdec" else 1  # kernels shared by Encaps and Decaps run once per op
+    if alg in HQ:
+        wk = hqc_work(alg)
+        once = name in ("k_hqc_dec_expand", "k_hqc_decode")  # Decaps-only kernels
+        c = 1 if once else calls
+        if name in wk["perms"]:
+            return c * wk["perms"][name] * PERM_OPS, "valu"
+        if name in wk["ops"]:
+            return c * wk["ops"][name], "valu"
+        return None, None
     if alg in FP:
         n = FP[alg][0]
         perms = frodo_perms(alg)
@@ -170,10 +205,10 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
     def run(n):
         if mode == "encdec":
             c, s = orc.batch_encaps(alg, take(pk, n), take(ec, n), threads)
-            return c, s, orc.batch_decaps(alg, take(sk, n), c, threads)
-        return None, None, orc.batch_decaps(alg, take(sk, n), take(ct_in, n), threads)
+            return c, s, orc.batch_decaps(alg, take(sk, n), c, threads, with_status=True)[0]
+        return None, None, orc.batch_decaps(alg, take(sk, n), take(ct_in, n), threads, with_status=True)[0]
 
-    cal = min(256 if alg in FP else 1024, B)
+    cal = min(256 if (alg in FP or alg in HQ) else 1024, B)
     t0 = time.perf_counter()
     run(cal)
     rate = cal / max(time.perf_counter() - t0, 1e-6)
@@ -196,10 +231,10 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
             cc, _ = orc.encaps(alg, pk_s[m].tobytes(), ec_s[m].tobytes())
         else:
             cc = ct_s[m].tobytes()
-        orc.decaps(alg, sk_s[m].tobytes(), cc)
+        orc.decaps_rc(alg, sk_s[m].tobytes(), cc)
         m += 1
     single = m / (time.perf_counter() - t0)
-    spec = "FrodoKEM round 3" if alg in FP else "FIPS 203"
+    spec = "FrodoKEM round 3" if alg in FP else ("HQC 2023-04-30" if alg in HQ else "FIPS 203")
     return {
         "value": S / dt, "unit": "encaps+decaps/s" if mode == "encdec" else "decaps/s", "cores": threads,
         "kind": "port",
@@ -324,16 +359,21 @@ def bench_handshake(args, world, rank, local):
     from qrkem.shard import reduce_run, weak_shard
     alg = args.alg
     frodo = alg in FP
-    lb = args.log2_batch if args.log2_batch is not None else (14 if frodo else 20)
+    hqc = alg in HQ
+    lb = args.log2_batch if args.log2_batch is not None else (14 if frodo else (16 if hqc else 20))
     B = 1 << lb
     drv = HandshakeDriver(alg, symmetric_name=args.symmetric, device=local, chunk=args.chunk)
     e = drv.engine
     base = weak_shard(rank, world, B).first
     kp, enc = e.kp_coins, e.enc_coins
-    coins = e.bench_coins(B, 2 * kp, args.seed, base)  # KeyGen coins (initiator | responder)
-    c_i, c_r = coins[:, :kp].contiguous(), coins[:, kp:].contiguous()
+    if 2 * kp <= 136:
+        coins = e.bench_coins(B, 2 * kp, args.seed, base)  # KeyGen coins (initiator | responder)
+        c_i, c_r = coins[:, :kp].contiguous(), coins[:, kp:].contiguous()
+        del coins
+    else:  # HQC: one SHAKE256 block per index and seed
+        c_i = e.bench_coins(B, kp, args.seed, base)
+        c_r = e.bench_coins(B, kp, args.seed ^ 0x5A5A, base)
     c_e = e.bench_coins(B, enc, args.seed ^ 0xE7C, base)  # Encaps coins: a second seed
-    del coins
     # peer p talks to this server node: infos differ per handshake (sorted ids, messaging.py:364-367)
     server = node_uuid("server-", rank)
     infos = [drv.info_for(node_uuid("peer-", base + i), server) for i in range(B)]
@@ -365,7 +405,7 @@ def bench_handshake(args, world, rank, local):
     disagree = int((out.agree != 1).sum().item())
     elapsed, (disagree,) = reduce_run(elapsed, [disagree], device=RED_DEVICE)
     value = B * world * args.steps / elapsed
-    W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric]) if not frodo else None
+    W = handshake_ops(alg, info_len, SYMMETRIC_KEY_SIZE[args.symmetric]) if not (frodo or hqc) else None
     kernels, roof = {}, None
     tot = sum(ms for ms, _ in prof.values()) or 1.0
     for name, (ms, cnt) in prof.items():
@@ -397,7 +437,7 @@ def bench_handshake(args, world, rank, local):
         import oracle as orc
         threads = cpu_threads()
         take = lambda t, n: np.ascontiguousarray(t[:n].cpu().numpy())  # noqa: E731
-        cal = min(B, 64 if frodo else 512)
+        cal = min(B, 64 if (frodo or hqc) else 512)
         t0 = time.perf_counter()
         orc.batch_handshake(alg, take(c_i, cal), take(c_r, cal), take(c_e, cal), infos[:cal], drv.key_len, threads)
         rate = cal / (time.perf_counter() - t0)
@@ -412,7 +452,8 @@ def bench_handshake(args, world, rank, local):
         result["cpu_baseline"] = {
             "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port",
             "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so: "
-                      f"{'FrodoKEM round 3' if frodo else 'FIPS 203'} + RFC 5869 C restatement, {threads} pthreads)",
+                      f"{'FrodoKEM round 3' if frodo else ('HQC 2023-04-30' if hqc else 'FIPS 203')} + RFC 5869 C "
+                      f"restatement, {threads} pthreads)",
             "sample_matches_gpu": match}
     if rank == 0:
         print(json.dumps(result))
@@ -547,7 +588,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--alg", default="ML-KEM-768")
-    ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM)")
+    ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM, HQC)")
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
@@ -586,7 +627,8 @@ def main():
     from qrkem.shard import reduce_run, weak_shard
     alg = args.alg
     frodo = alg in FP
-    lb = args.log2_batch if args.log2_batch is not None else (16 if frodo else 20)
+    hqc = alg in HQ
+    lb = args.log2_batch if args.log2_batch is not None else (16 if (frodo or hqc) else 20)
     B = 1 << lb
     eng = BatchKEM(alg, device=local, chunk=args.chunk)
     if args.streams:
@@ -597,10 +639,14 @@ def main():
     base = weak_shard(rank, world, B).first  # global index range [base, base + B)
 
     kpl, encl = eng.kp_coins, eng.enc_coins
-    coins = eng.bench_coins(B, kpl + encl, args.seed, base)
-    kc = coins[:, :kpl].contiguous()
-    ec = coins[:, kpl:].contiguous()
-    del coins
+    if kpl + encl <= 136:  # one SHAKE256 block per index
+        coins = eng.bench_coins(B, kpl + encl, args.seed, base)
+        kc = coins[:, :kpl].contiguous()
+        ec = coins[:, kpl:].contiguous()
+        del coins
+    else:  # HQC-192/256: KeyGen and Encaps coins from two seeds
+        kc = eng.bench_coins(B, kpl, args.seed, base)
+        ec = eng.bench_coins(B, encl, args.seed ^ 0xE7C, base)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pk, sk = eng.keypair(coins=kc)
@@ -671,6 +717,9 @@ def main():
         variants["mixed"] = elapsed * 1e3 / args.steps
         tampered = (ct != cts["all-valid"]).any(dim=1)
         same = (ss2 == ss).all(dim=1)
+        if hqc:  # the per-record return code must flag exactly the tampered rows
+            _, st = eng.decaps(sk, cts["mixed"], return_status=True)
+            checks["status_mismatches"] = int(((st != 0) != tampered).sum().item())
         # valid rows must give the encapsulated key, tampered rows the implicit-rejection key
         bad = int((same != ~tampered).sum().item())
         counters = [bad, int(tampered.sum().item())]
@@ -708,6 +757,7 @@ def main():
     W = valu_ops(alg, args.mode)
     headline = alg == "ML-KEM-768" and args.mode == "encdec"
     cfg_idx = (2 if lb >= 24 else 1) if not frodo and args.mode == "encdec" else (3 if frodo else 4)
+    cfg_label = "SURVEY.md 8f-4" if hqc else f"BASELINE.json configs[{cfg_idx}]"
     what = "Encaps+Decaps" if args.mode == "encdec" else "Decaps, 50% tampered (mixed)"
     result = {
         "metric": METRIC if headline else f"{alg} {'encaps+decaps' if args.mode == 'encdec' else 'decaps'}"
@@ -721,11 +771,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32" if not frodo else ("u32 (AES T-table) + i8->i32 (MFMA)" if alg.endswith("-AES") else "u32 (Keccak) + i8->i32 (MFMA)"),
+        "dtype": "u32 (Keccak, F2[X] words, GF(2^8))" if hqc else "u32" if not frodo else ("u32 (AES T-table) + i8->i32 (MFMA)" if alg.endswith("-AES") else "u32 (Keccak) + i8->i32 (MFMA)"),
         "data": "synthetic: coins = SHAKE256('qrk-bench'||LE64(seed)||LE64(i)) generated on device; "
                 "keys from batched KeyGen on those coins",
         "config": {"workload": f"{alg} {what} of 2^{lb} device-resident handshakes per GPU "
-                               f"(BASELINE.json configs[{cfg_idx}])",
+                               f"({cfg_label})",
                    "alg": alg, "batch_per_gpu": B, "global_batch": B * world, "chunk": chunk_eff,
                    "parallelism": f"index-sharded x{world} (no data-path collective)"},
         "roofline": roof,

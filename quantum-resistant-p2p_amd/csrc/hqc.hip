@@ -32,16 +32,18 @@ namespace hqc {
 
 constexpr int SEED = 40, SALT = 16, SSB = 64;
 
-template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_>
+// TPB threads per handshake in the workgroup kernels, WPT output words per thread (odd, so a
+// wave's contiguous WPT+1-word windows fall on distinct LDS banks)
+template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_, int TPB_>
 struct Params {
   static constexpr int N = N_, N1 = N1_, N2 = N2_, W = W_, WR = WR_, WE = WE_, K = K_, DELTA = DELTA_,
-                       MULT = MULT_, WPT = WPT_;
+                       MULT = MULT_, WPT = WPT_, TPB = TPB_;
   static constexpr int NB = (N + 7) / 8, VB = N1 * N2 / 8;
   static constexpr int NW32 = (N + 31) / 32, VW32 = VB / 4, N32 = N >> 5, NR = N & 31;
   static constexpr int NHW = (NB + 7) / 8;  // h stream words (the seedexpander squeezes 8-byte units)
   static constexpr int PK = SEED + NB, SK = SEED + K + PK, CT = NB + VB + SALT, KPC = 2 * SEED + K, ENC = K + SALT;
   static constexpr int RWW = (4 * W + 7) / 8, RWR = (4 * WR + 7) / 8, RWE = (4 * WE + 7) / 8;
-  static constexpr int NWP = 256 * WPT, NH2 = NWP + N32 + 2;
+  static constexpr int NWP = TPB * WPT, NH2 = NWP + N32 + 2;
   static constexpr int MSGB = K + NB + VB, MW = (MSGB + 2 + 7) / 8;  // K-hash message || 0x05 || 0x1F, words
   static constexpr int MBW = ((SK > 8 * MW ? SK : 8 * MW) + 15) / 4;  // LDS byte buffer, words
   static constexpr int T2 = 2 * DELTA, WMAX = W > WR ? W : WR;
@@ -50,11 +52,12 @@ struct Params {
   static_assert(NR != 0, "n is never a multiple of 32 for HQC");
   static_assert(T2 + 1 <= 64 && WMAX <= 192 && N1 <= 128, "lane mappings");
   static_assert(NWP >= NW32, "WPT too small");
+  static_assert(WPT % 2 == 1 && TPB % 64 == 0 && TPB >= 256, "bank-conflict-free windows; >= 4 waves");
 };
 template <int L> struct HQ;
-template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 3> {};
-template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 5> {};
-template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 8> {};
+template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 3, 256> {};
+template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 5, 256> {};
+template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 5, 384> {};
 
 // ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
 struct GfTabs {
@@ -289,7 +292,7 @@ template <int L>
 __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, uint32_t* sup) {
   using P = HQ<L>;
   const uint32_t* r32 = (const uint32_t*)words;
-  for (int i = threadIdx.x; i < weight; i += 256)
+  for (int i = threadIdx.x; i < weight; i += P::TPB)
     sup[i] = (uint32_t)i + __umulhi(r32[i], (uint32_t)(P::N - i));
 }
 
@@ -328,7 +331,7 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
     const uint32_t v = rd(j);
     return j == P::NW32 - 1 ? (v & TOPMASK) : v;
   };
-  for (int q = threadIdx.x; q < P::NH2; q += 256) {
+  for (int q = threadIdx.x; q < P::NH2; q += P::TPB) {
     uint32_t v = q < P::NW32 ? rd(q) : 0u;
     if (q >= P::N32) v ^= alignbit(clean(q - P::N32), clean(q - P::N32 - 1), 32 - P::NR);
     D[q] = v;
@@ -382,13 +385,13 @@ __device__ __forceinline__ void lds_store_u32_unaligned(uint8_t* b, int off, uin
 }
 
 __device__ __forceinline__ void fill_gf(uint8_t* e, uint8_t* l) {
-  for (int i = threadIdx.x; i < 512; i += 256) e[i] = GF.exp[i];
-  for (int i = threadIdx.x; i < 256; i += 256) l[i] = GF.log[i];
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) e[i] = GF.exp[i];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) l[i] = GF.log[i];
 }
 
 // ---------------------------------------------------------------- KeyGen: s = x + y h
 template <int L>
-__global__ __launch_bounds__(256) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ coins, uint8_t* __restrict__ pk,
                                                     uint8_t* __restrict__ sk) {
   using P = HQ<L>;
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(256) void k_hqc_kg_mul(size_t n, const uint64_t* __
   supports_raw<L>(rw, P::W, SX);
   supports_raw<L>(rw + P::RWW, P::W, SY);
   // sk = sk_seed || sigma || pk_seed || s  (the coins' first 80 + K bytes, in order)
-  for (int b = t; b < P::KPC; b += 256) mb[b] = c[b];
+  for (int b = t; b < P::KPC; b += P::TPB) mb[b] = c[b];
   __syncthreads();
   if (wave == 0) dedupe_wave(SX, P::W);
   if (wave == 1) dedupe_wave(SY, P::W);
@@ -419,15 +422,15 @@ __global__ __launch_bounds__(256) void k_hqc_kg_mul(size_t n, const uint64_t* __
 #pragma unroll
   for (int q = 0; q < P::WPT; ++q) D[j0 + q] = acc[0][q];
   __syncthreads();
-  for (int i = t; i < P::W; i += 256) atomicXor(&D[SX[i] >> 5], 1u << (SX[i] & 31));
+  for (int i = t; i < P::W; i += P::TPB) atomicXor(&D[SX[i] >> 5], 1u << (SX[i] & 31));
   __syncthreads();
   constexpr int SOFF = (2 * SEED + P::K) / 4;  // s at byte 80 + K (a multiple of 4)
-  for (int j = t; j < P::NW32; j += 256) MB[SOFF + j] = j == P::NW32 - 1 ? (D[j] & ((1u << P::NR) - 1)) : D[j];
+  for (int j = t; j < P::NW32; j += P::TPB) MB[SOFF + j] = j == P::NW32 - 1 ? (D[j] & ((1u << P::NR) - 1)) : D[j];
   __syncthreads();
   uint8_t* so = sk + hs * P::SK;
   uint8_t* po = pk + hs * P::PK;
-  for (int b = t; b < P::SK; b += 256) so[b] = mb[b];
-  for (int b = t; b < P::PK; b += 256) po[b] = mb[SEED + P::K + b];
+  for (int b = t; b < P::SK; b += P::TPB) so[b] = mb[b];
+  for (int b = t; b < P::PK; b += P::TPB) po[b] = mb[SEED + P::K + b];
 }
 
 // ---------------------------------------------------------------- Encaps / re-encryption
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(256) void k_hqc_kg_mul(size_t n, const uint64_t* __
 // Decaps re-encryption (REENC = true): m' from mp; s and sigma from sk; compares (u', v') with the
 // received ct; message = (m' if equal else sigma) || u || v of the received ct; status -1 if unequal.
 template <int L, bool REENC>
-__global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
                                                      const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ ct_out, const uint8_t* __restrict__ mp,
                                                      const uint8_t* __restrict__ sk, const uint8_t* __restrict__ ct_in,
@@ -455,7 +458,7 @@ __global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* _
   // phase A: h doubled, s staged (bytes), supports, m, GF tables
   const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });
-  for (int b = t; b < 4 * P::NW32; b += 256) mb[b] = b < P::NB ? spk[SEED + b] : 0;
+  for (int b = t; b < 4 * P::NW32; b += P::TPB) mb[b] = b < P::NB ? spk[SEED + b] : 0;
   supports_raw<L>(rw, P::WR, S1);
   supports_raw<L>(rw + P::RWR, P::WR, S2);
   supports_raw<L>(rw + 2 * P::RWR, P::WE, SE);
@@ -493,8 +496,8 @@ __global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* _
 #pragma unroll
   for (int q = 0; q < P::WPT; ++q) D1[j0 + q] = acc[0][q], D2[j0 + q] = acc[1][q];
   __syncthreads();
-  for (int i = t; i < P::WR; i += 256) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
-  for (int i = t; i < P::WE; i += 256) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
+  for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
+  for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
   __syncthreads();
   constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
   constexpr int UOFF = P::K / 4;  // u at message byte K
@@ -503,17 +506,17 @@ __global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* _
     return D2[j] ^ rm_word(SYM[sym], j & 3);
   };
   if constexpr (!REENC) {
-    for (int j = t; j < P::NW32; j += 256) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
+    for (int j = t; j < P::NW32; j += P::TPB) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
     if (t < P::K) mb[t] = MM[t];
     __syncthreads();  // the last u word's spare bytes are v's first bytes
-    for (int j = t; j < P::VW32; j += 256) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
+    for (int j = t; j < P::VW32; j += P::TPB) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
   } else {
     // received u || v into the message area, then compare with the re-encryption
     const uint8_t* cin = ct_in + hs * P::CT;
-    for (int b = t; b < P::NB + P::VB; b += 256) mb[P::K + b] = cin[b];
+    for (int b = t; b < P::NB + P::VB; b += P::TPB) mb[P::K + b] = cin[b];
     __syncthreads();
     uint32_t diff = 0;
-    for (int j = t; j < P::NW32; j += 256) {
+    for (int j = t; j < P::NW32; j += P::TPB) {
       uint32_t u = D1[j], c = MB[UOFF + j];
       if (j == P::NW32 - 1) {
         u &= TOPMASK;
@@ -523,29 +526,29 @@ __global__ __launch_bounds__(256) void k_hqc_enc_mul(size_t n, const uint64_t* _
       }
       diff |= u ^ c;
     }
-    for (int j = t; j < P::VW32; j += 256) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
+    for (int j = t; j < P::VW32; j += P::TPB) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
     if (diff) atomicOr(&DIFF, 1u);
     __syncthreads();
     const bool ok = DIFF == 0;
     if (t < P::K) mb[t] = ok ? MM[t] : sk[hs * P::SK + SEED + t];
     if (t == 0) status[hs] = ok ? 0 : -1;
   }
-  for (int b = P::MSGB + t; b < 8 * P::MW; b += 256) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
+  for (int b = P::MSGB + t; b < 8 * P::MW; b += P::TPB) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
   __syncthreads();
   // phase E: K-hash message rows (aligned words), ciphertext bytes
   const uint64_t* m64 = (const uint64_t*)MB;
   uint64_t* mo = msg + hs * P::MW;
-  for (int w = t; w < P::MW; w += 256) mo[w] = m64[w];
+  for (int w = t; w < P::MW; w += P::TPB) mo[w] = m64[w];
   if constexpr (!REENC) {
     uint8_t* co = ct_out + hs * P::CT;
-    for (int b = t; b < P::NB + P::VB; b += 256) co[b] = mb[P::K + b];
+    for (int b = t; b < P::NB + P::VB; b += P::TPB) co[b] = mb[P::K + b];
     if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
   }
 }
 
 // ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
 template <int L>
-__global__ __launch_bounds__(256) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ ct, uint8_t* __restrict__ mp) {
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2];
@@ -559,8 +562,8 @@ __global__ __launch_bounds__(256) void k_hqc_decode(size_t n, const uint64_t* __
   const uint64_t* rw = row + hs * P::ROWW;
   uint8_t* mb = (uint8_t*)MB;
   const uint8_t* c = ct + hs * P::CT;
-  for (int b = t; b < 4 * P::NW32; b += 256) mb[b] = b < P::NB + P::VB ? c[b] : 0;
-  for (int b = 4 * P::NW32 + t; b < P::NB + P::VB; b += 256) mb[b] = c[b];
+  for (int b = t; b < 4 * P::NW32; b += P::TPB) mb[b] = b < P::NB + P::VB ? c[b] : 0;
+  for (int b = 4 * P::NW32 + t; b < P::NB + P::VB; b += P::TPB) mb[b] = c[b];
   supports_raw<L>(rw + P::RWW, P::W, SY);
   fill_gf(GE, GL);
   __syncthreads();
@@ -581,7 +584,7 @@ __global__ __launch_bounds__(256) void k_hqc_decode(size_t n, const uint64_t* __
   }
   __syncthreads();
   // duplicated RM(1,7): one wave per symbol, lane l holds positions l and l + 64
-  for (int sym = wave; sym < P::N1; sym += 4) {
+  for (int sym = wave; sym < P::N1; sym += P::TPB / 64) {
     const uint32_t* cw = T + sym * 4 * P::MULT;
     int x0 = 0, x1 = 0;
 #pragma unroll
@@ -716,7 +719,7 @@ template <int L>
 hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
   View v = carve<L>(scratch, n);
   QRK_LAUNCH("k_hqc_kg_expand", st, k_hqc_kg_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, v.row);
-  QRK_LAUNCH("k_hqc_kg_mul", st, k_hqc_kg_mul<L>, dim3((unsigned)n), dim3(256), 0, st, n, v.row, coins, pk, sk);
+  QRK_LAUNCH("k_hqc_kg_mul", st, k_hqc_kg_mul<L>, dim3((unsigned)n), dim3(HQ<L>::TPB), 0, st, n, v.row, coins, pk, sk);
   return hipGetLastError();
 }
 
@@ -727,7 +730,7 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   View v = carve<L>(scratch, n);
   QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins,
              (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, v.row);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(256), 0, st, n, v.row, coins,
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, coins,
              pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
              v.msg);
   QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
@@ -741,10 +744,10 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   View v = carve<L>(scratch, n);
   int32_t* stp = status ? status : v.st;
   QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.row);
-  QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(256), 0, st, n, v.row, ct, v.mp);
+  QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, ct, v.mp);
   QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.mp, (size_t)32,
              sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(256), 0, st, n, v.row,
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row,
              (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
   QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
   return hipGetLastError();
