@@ -156,6 +156,13 @@ int qrk_bench_coins(qrk_ctx *ctx, size_t n, size_t len, uint64_t seed, uint64_t 
 /* Flip one ciphertext bit per selected index (mode 0 none, 1 all, 2 Bernoulli(1/2)):
  * h_i = SHAKE256("qrk-tamper"||LE64(seed)||LE64(i))[0..8), bit (h_i>>1) mod 8*ctlen. */
 int qrk_tamper(qrk_ctx *ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t *ct, void *stream);
+/* HQC fixed-weight supports (the sampling inside KeyGen / Encaps / Decaps, exposed so the
+ * duplicate-removal step can be tested on inputs crafted to collide): for each of n vectors,
+ * sup[v][i] = i + floor(r[v][i] * (n_HQC - i) / 2^32), then the spec's removal of duplicates.
+ * kind 0: weight w (x, y), kind 1: weight w_r = w_e (r1, r2, e).  Device uint32 pointers,
+ * [n][weight] each. */
+int qrk_hqc_supports(qrk_ctx *ctx, const char *alg, int kind, size_t n, const uint32_t *r, uint32_t *sup,
+                     void *stream);
 
 /* HKDF-SHA256 (RFC 5869) over n keys, one GPU lane per key.  Replaces
  * SecureMessaging._derive_symmetric_key (messaging.py:350-382: HKDF(SHA256,

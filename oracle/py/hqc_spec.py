@@ -134,7 +134,14 @@ def shake_ds(data: bytes, domain: int) -> bytes:
 def fixed_weight_support(se: SeedExpander, n: int, weight: int) -> list[int]:
     raw = se.read(4 * weight)
     r = [int.from_bytes(raw[4 * i:4 * i + 4], "little") for i in range(weight)]
-    s = [i + ((r[i] * (n - i)) >> 32) for i in range(weight)]
+    return remove_duplicates([i + ((r[i] * (n - i)) >> 32) for i in range(weight)])
+
+
+def remove_duplicates(s: list[int]) -> list[int]:
+    """The spec's serial duplicate removal (vect_set_random_fixed_weight, 2023-04-30):
+    for i = w-2 .. 0, s_i := i when s_i equals some s_j with j > i."""
+    s = list(s)
+    weight = len(s)
     for i in range(weight - 2, -1, -1):
         if any(s[j] == s[i] for j in range(i + 1, weight)):
             s[i] = i

@@ -684,6 +684,17 @@ int qrk_tamper(qrk_ctx* ctx, size_t n, size_t ctlen, uint64_t seed, int mode, ui
   return e == hipSuccess ? 0 : hip_fail("tamper", e);
 }
 
+int qrk_hqc_supports(qrk_ctx* ctx, const char* alg, int kind, size_t n, const uint32_t* r, uint32_t* sup,
+                     void* stream) {
+  QRK_RESOLVE(ctx, alg);
+  if (a->family != Family::HQC) return fail(std::string("not an HQC parameter set: ") + alg);
+  if (kind != 0 && kind != 1) return fail("kind must be 0 (w) or 1 (w_r = w_e)");
+  if (n && (!r || !sup)) return fail("null buffer");
+  if (ensure_device(ctx->device)) return -1;
+  hipError_t e = hqc_supports(*a, kind, n, r, sup, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("hqc_supports", e);
+}
+
 int qrk_hkdf_sha256_batch(qrk_ctx* ctx, size_t n, const uint8_t* ikm, size_t ikm_len, const uint8_t* salt,
                           size_t salt_len, const uint8_t* info, const uint64_t* info_off, size_t info_len,
                           uint8_t* okm, size_t okm_len, void* stream) {

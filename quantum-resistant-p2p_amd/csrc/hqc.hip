@@ -296,28 +296,49 @@ __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, 
     sup[i] = (uint32_t)i + __umulhi(r32[i], (uint32_t)(P::N - i));
 }
 
-// one wave: for i = weight-2 .. 0, s_i := i when s_i equals some s_j with j > i (branch-free;
-// lanes hold j = lane, lane + 64, lane + 128)
-__device__ __forceinline__ void dedupe_wave(uint32_t* sup, int weight) {
-  const int lane = threadIdx.x & 63;
-  uint32_t f[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) f[q] = (lane + 64 * q < weight) ? sup[lane + 64 * q] : 0xFFFFFFFFu;
-#pragma unroll 1
-  for (int i = weight - 2; i >= 0; --i) {
-    const int qi = i >> 6, li = i & 63;
-    const uint32_t oi = __builtin_amdgcn_readlane(qi == 0 ? f[0] : (qi == 1 ? f[1] : f[2]), li);
-    bool hit = false;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) hit |= (lane + 64 * q > i) && (f[q] == oi);
-    const bool found = __ballot(hit) != 0;
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (found && lane + 64 * q == i) f[q] = (uint32_t)i;
+// The spec's duplicate removal (oracle/src/hqc.c fixed_weight): for i = w-2 .. 0, s_i := i when
+// s_i equals some s_j with j > i.  That serial loop has a closed form (tests/test_hqc_dedupe.py
+// checks it against the loop): s_i is replaced iff
+//   s_j == s_i for some j > i   (the original values; every lower copy of a value is replaced), or
+//   i < s_i < w and s_{s_i} is replaced   (s_i collides with the index written at j = s_i).
+// The second term is a chain through strictly increasing indices; pointer jumping resolves it in
+// ceil(log2 w) rounds.  All threads of the workgroup take part, no data-dependent control flow.
+// NV supports of weight WT, vector v at SS + v * WMAX; PJ: NV * WT words of scratch
+// (bit 31 = replaced so far along the chain, low 16 bits = next chain index or NONE).
+template <int L, int NV, int WT>
+__device__ __forceinline__ void dedupe_wg(uint32_t* SS, uint32_t* PJ) {
+  using P = HQ<L>;
+  constexpr uint32_t NONE = 0xFFFFu, REP = 0x80000000u;
+  constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);  // 2^ROUNDS >= WT chain nodes
+  static_assert(WT <= P::WMAX && WT > 1, "weight");
+  for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
+    const int v = e / WT, i = e - v * WT;
+    const uint32_t* s = SS + v * P::WMAX;
+    const uint32_t o = s[i];
+    uint32_t dup = 0;
+#pragma unroll 8
+    for (int j = 0; j < WT; ++j) dup |= (uint32_t)((j > i) & (s[j] == o));
+    const uint32_t ptr = (o > (uint32_t)i && o < (uint32_t)WT) ? o : NONE;
+    PJ[e] = (dup ? REP : 0u) | ptr;
   }
-#pragma unroll
-  for (int q = 0; q < 3; ++q)
-    if (lane + 64 * q < weight) sup[lane + 64 * q] = f[q];
+  __syncthreads();
+  // in place: a node read mid-round is either its old or its new (rep, ptr) pair, both of which
+  // keep "rep = OR over the chain from here up to ptr"; jumps still at least double per round
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
+    for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
+      const int v = e / WT, i = e - v * WT;
+      const uint32_t x = PJ[e], p = x & NONE;
+      const uint32_t y = PJ[v * WT + (p == NONE ? i : (int)p)];
+      PJ[e] = (x & REP) | y;
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
+    const int v = e / WT, i = e - v * WT;
+    if (PJ[e] & REP) SS[v * P::WMAX + i] = (uint32_t)i;
+  }
+  __syncthreads();
 }
 
 // doubled dense operand: D[q] = raw[q] ^ (clean << n)[q], raw words via rd(j) (0 outside [0, NW32)),
@@ -397,10 +418,12 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   using P = HQ<L>;
   __shared__ uint32_t D[P::NH2];
   __shared__ uint32_t MB[P::MBW];
-  __shared__ uint32_t SX[P::WMAX], SY[P::WMAX];
+  __shared__ uint32_t SS[2 * P::WMAX], PJ[2 * P::W];
+  uint32_t* const SX = SS;
+  uint32_t* const SY = SS + P::WMAX;
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
-  const int t = threadIdx.x, wave = t >> 6;
+  const int t = threadIdx.x;
   const uint64_t* rw = row + hs * P::ROWW;
   const uint8_t* c = coins + hs * P::KPC;
   uint8_t* mb = (uint8_t*)MB;
@@ -411,9 +434,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   // sk = sk_seed || sigma || pk_seed || s  (the coins' first 80 + K bytes, in order)
   for (int b = t; b < P::KPC; b += P::TPB) mb[b] = c[b];
   __syncthreads();
-  if (wave == 0) dedupe_wave(SX, P::W);
-  if (wave == 1) dedupe_wave(SY, P::W);
-  __syncthreads();
+  dedupe_wg<L, 2, P::W>(SS, PJ);
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D};
   sparse_dense<L, 1>(SY, P::W, Ds, acc);
@@ -446,7 +467,11 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2], D2[P::NH2];
   __shared__ __attribute__((aligned(16))) uint32_t MB[P::MBW];
-  __shared__ uint32_t S1[P::WMAX], S2[P::WMAX], SE[P::WMAX];
+  __shared__ uint32_t SS[3 * P::WMAX], PJ[3 * P::WR];
+  uint32_t* const S1 = SS;
+  uint32_t* const S2 = SS + P::WMAX;
+  uint32_t* const SE = SS + 2 * P::WMAX;
+  static_assert(P::WR == P::WE, "one dedupe over r1, r2, e");
   __shared__ uint8_t GE[512], GL[256], SYM[128], MM[32];
   __shared__ uint32_t DIFF;
   const size_t hs = blockIdx.x;
@@ -466,11 +491,8 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   if (t < P::K) MM[t] = REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t];
   if (t == 0) DIFF = 0;
   __syncthreads();
-  // phase B: s doubled (keeps stray bits of a malformed pk), dedupe, RS parity
+  // phase B: s doubled (keeps stray bits of a malformed pk), RS parity, dedupe
   build_doubled<L>(D2, [&](int j) { return MB[j]; });
-  if (wave == 0) dedupe_wave(S1, P::WR);
-  if (wave == 1) dedupe_wave(S2, P::WR);
-  if (wave == 2) dedupe_wave(SE, P::WE);
   if (wave == 3) {
     const RsTab<L>& rs = rs_tab<L>();
     if (lane < P::T2) {
@@ -486,7 +508,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
     }
     if (lane + 64 < P::N1) SYM[lane + 64] = MM[lane + 64 - P::T2];
   }
-  __syncthreads();
+  dedupe_wg<L, 3, P::WR>(SS, PJ);  // ends with a barrier
   // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
   uint32_t acc[2][P::WPT] = {};
   const uint32_t* const Ds[2] = {D1, D2};
@@ -554,7 +576,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   __shared__ uint32_t D1[P::NH2];
   __shared__ uint32_t T[P::NWP];
   __shared__ uint32_t MB[(P::NB + P::VB + 8) / 4 + 1];
-  __shared__ uint32_t SY[P::WMAX];
+  __shared__ uint32_t SY[P::WMAX], PJ[P::W];
   __shared__ uint8_t GE[512], GL[256], SYM[128], SYN[64], CL[64], OM[64];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
@@ -571,8 +593,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
   constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? (MB[j] & BM) : MB[j]; });
-  if (wave == 0) dedupe_wave(SY, P::W);
-  __syncthreads();
+  dedupe_wg<L, 1, P::W>(SY, PJ);
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D1};
   sparse_dense<L, 1>(SY, P::W, Ds, acc);
@@ -685,6 +706,31 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   if (lane < P::K) mp[hs * 32 + lane] = SYM[P::T2 + lane];
 }
 
+// ---------------------------------------------------------------- fixed-weight supports alone
+// (test hook behind qrk_hqc_supports: r words -> deduplicated supports, one workgroup per vector)
+template <int L, int WT>
+__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_supports(size_t n, const uint32_t* __restrict__ r,
+                                                      uint32_t* __restrict__ sup) {
+  using P = HQ<L>;
+  __shared__ uint32_t SS[P::WMAX], PJ[WT];
+  const size_t v = blockIdx.x;
+  if (v >= n) return;
+  for (int i = threadIdx.x; i < WT; i += P::TPB) SS[i] = (uint32_t)i + __umulhi(r[v * WT + i], (uint32_t)(P::N - i));
+  __syncthreads();
+  dedupe_wg<L, 1, WT>(SS, PJ);
+  for (int i = threadIdx.x; i < WT; i += P::TPB) sup[v * WT + i] = SS[i];
+}
+
+template <int L>
+hipError_t supports_t(int kind, size_t n, const uint32_t* r, uint32_t* sup, hipStream_t st) {
+  using P = HQ<L>;
+  if (kind == 0)
+    QRK_LAUNCH("k_hqc_supports", st, (k_hqc_supports<L, P::W>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, r, sup);
+  else
+    QRK_LAUNCH("k_hqc_supports", st, (k_hqc_supports<L, P::WR>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, r, sup);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 inline unsigned blocks_for(size_t t) { return (unsigned)((t + 255) / 256); }
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -781,6 +827,16 @@ hipError_t hqc_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, cons
     case 128: return hqc::encaps_t<128>(n, ct, ss, pk, coins, scratch, s.main);
     case 192: return hqc::encaps_t<192>(n, ct, ss, pk, coins, scratch, s.main);
     case 256: return hqc::encaps_t<256>(n, ct, ss, pk, coins, scratch, s.main);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t hqc_supports(const AlgInfo& a, int kind, size_t n, const uint32_t* r, uint32_t* sup, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 128: return hqc::supports_t<128>(kind, n, r, sup, st);
+    case 192: return hqc::supports_t<192>(kind, n, r, sup, st);
+    case 256: return hqc::supports_t<256>(kind, n, r, sup, st);
   }
   return hipErrorInvalidValue;
 }

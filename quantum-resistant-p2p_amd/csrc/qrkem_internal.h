@@ -84,6 +84,9 @@ hipError_t hqc_encaps(const AlgInfo& a, size_t n, uint8_t* ct, uint8_t* ss, cons
                       void* scratch, const Streams& st);
 hipError_t hqc_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, int32_t* status,
                       void* scratch, const Streams& st);
+// Fixed-weight supports from n vectors of random words r[n][w] (kind 0: w = the key weight,
+// 1: w = the encryption weight w_r = w_e): sup_i = i + floor(r_i (n - i) / 2^32), deduplicated.
+hipError_t hqc_supports(const AlgInfo& a, int kind, size_t n, const uint32_t* r, uint32_t* sup, hipStream_t st);
 
 // SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len) for i < n, len <= 136.
 hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st);

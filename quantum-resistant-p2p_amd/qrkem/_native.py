@@ -55,6 +55,7 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_kem_decaps_batch_status_host": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P]),
         "qrk_bench_coins": (ct.c_int, [P, SZ, SZ, ct.c_uint64, ct.c_uint64, P, P]),
         "qrk_tamper": (ct.c_int, [P, SZ, SZ, ct.c_uint64, ct.c_int, P, P]),
+        "qrk_hqc_supports": (ct.c_int, [P, ct.c_char_p, ct.c_int, SZ, P, P, P]),
         "qrk_hkdf_sha256_batch": (ct.c_int, [P, SZ, P, SZ, P, SZ, P, P, SZ, P, SZ, P]),
         "qrk_handshake_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P, P, SZ, SZ, P, P, P, P, P, P, P]),
         "qrk_base64_encode_batch": (ct.c_int, [P, SZ, P, SZ, P, P]),

@@ -207,3 +207,11 @@ class BatchKEM:
         """In-place: mode 0 none, 1 every ciphertext, 2 Bernoulli(1/2) per index."""
         self._check(LIB.qrk_tamper(self._ctx, ct_.shape[0], self.ct_len, seed, mode, _dptr(ct_), self._stream()),
                     "tamper")
+
+    def hqc_supports(self, r, kind: int):
+        """HQC fixed-weight supports from device uint32 random words r [n][weight] (kind 0: w,
+        1: w_r = w_e), duplicates removed as the spec does (test hook, qrk_hqc_supports)."""
+        out = torch.empty_like(r)
+        self._check(LIB.qrk_hqc_supports(self._ctx, self.alg.encode(), kind, r.shape[0], _dptr(r), _dptr(out),
+                                          self._stream()), "hqc_supports")
+        return out

@@ -168,3 +168,36 @@ def test_plugin_single_shot(level, alg):
     bad[100] ^= 4
     with pytest.raises(RuntimeError):
         kem.decapsulate(sk, bytes(bad))
+
+
+def _r_for(sup, n):
+    """random words r_i with i + floor(r_i (n - i) / 2^32) = sup_i (needs i <= sup_i < n)"""
+    r = [-(-((s - i) << 32) // (n - i)) for i, s in enumerate(sup)]
+    assert all(i + ((x * (n - i)) >> 32) == s for i, (x, s) in enumerate(zip(r, sup)))
+    return r
+
+
+@pytest.mark.parametrize("alg", ALGS)
+def test_supports_duplicate_removal(engines, alg):
+    """qrk_hqc_supports on supports crafted to collide (value duplicates, index collisions, a
+    chain through every index) vs the spec's serial loop (hqc_spec.remove_duplicates)."""
+    import random
+
+    import hqc_spec as H
+    p = H.params(alg)
+    n = p["n"]
+    rng = random.Random(n)
+    for kind, w in ((0, p["w"]), (1, p["wr"])):
+        sups = [
+            [i + rng.randrange(4) for i in range(w)],
+            [w + 5] * w,
+            [i + 1 for i in range(w - 1)] + [w - 1],
+            [rng.randrange(i, 2 * w) for i in range(w)],
+            [rng.randrange(i, n) for i in range(w)],
+            [n - 1] * w,
+            list(range(w)),
+        ]
+        r = np.array([_r_for(s, n) for s in sups], dtype=np.uint32)
+        got = _host(engines[alg].hqc_supports(_dev(r.view(np.int32)), kind)).view(np.uint32)
+        for s, g in zip(sups, got):
+            assert list(g) == H.remove_duplicates(s)
