@@ -199,10 +199,11 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
 #define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
 
-// (a & m) | b as one v_and_or_b32 (LLVM rewrites a disjoint OR into and + add)
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
+// (a & m) | b as one v_bitop3_b32 (truth table 0xEA): full rate on gfx950, where
+// v_and_or_b32 issues at half rate (profiles/r1/valu_peak_r1b.json)
+__device__ __forceinline__ uint32_t and_or3(uint32_t a, uint32_t m, uint32_t b) {
   uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(b));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(a), "s"(m), "v"(b));
   return r;
 }
 // (a << s) | b as one v_lshl_or_b32
@@ -215,7 +216,7 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 // Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
 // flushing completed 8-coefficient chunks to dst.
 // `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
-// 8-11 are zero, so an entry address is one v_and_or_b32, (pos & 0xF00) | rb, with the static
+// 8-11 are zero, so an entry address is one v_bitop3_b32, (pos & 0xF00) | rb, with the static
 // LDS base folded into the ds_write offset.
 __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
@@ -235,7 +236,7 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     int pos = cnt << 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      *(uint32_t*)(ring_all + and_or(pos, 0xF00u, rb)) = (uint32_t)c[e];
+      *(uint32_t*)(ring_all + and_or3(pos, 0xF00u, rb)) = (uint32_t)c[e];
       pos += c[e] < Q ? 256 : 0;
     }
     cnt = pos >> 8;
