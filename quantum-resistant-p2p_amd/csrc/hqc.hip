@@ -11,8 +11,8 @@
 //   k_hqc_kg_mul      WG / hs     s = x + y h; pk = pk_seed || s; sk = sk_seed || sigma || pk
 //   k_hqc_enc_mul     WG / hs     u = r1 + r2 h, v = C.encode(m) + r2 s + e (truncated); ct; K-hash message
 //                                 (REENC: the same re-encryption inside Decaps, compared with the received ct)
-//   k_hqc_decode      WG / hs     v - u y, duplicated RM(1,7) decoding (wave-wide Hadamard transform),
-//                                 RS decoding (syndromes, Berlekamp-Massey, Chien, Forney) -> m'
+//   k_hqc_decode      WG / hs     v - u y, duplicated RM(1,7) decoding (wave-wide Hadamard transform) -> symbols
+//   k_hqc_rs          wave / hs   RS decoding (syndromes, Berlekamp-Massey, Chien, Forney) -> m'
 //   k_hqc_hash        lane / hs   ss = SHAKE256(m || u || v || 0x05)
 //
 // The sparse-dense products in F2[X]/(X^n - 1) run one workgroup (256 threads) per handshake.
@@ -571,13 +571,14 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
 // ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
 template <int L>
 __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
-                                                    const uint8_t* __restrict__ ct, uint8_t* __restrict__ mp) {
+                                                    const uint8_t* __restrict__ ct, uint8_t* __restrict__ syms,
+                                                    size_t sym_stride) {
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2];
   __shared__ uint32_t T[P::NWP];
   __shared__ uint32_t MB[(P::NB + P::VB + 8) / 4 + 1];
   __shared__ uint32_t SY[P::WMAX], PJ[P::W];
-  __shared__ uint8_t GE[512], GL[256], SYM[128], SYN[64], CL[64], OM[64];
+  __shared__ uint8_t SYM[128];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -587,7 +588,6 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   for (int b = t; b < 4 * P::NW32; b += P::TPB) mb[b] = b < P::NB + P::VB ? c[b] : 0;
   for (int b = 4 * P::NW32 + t; b < P::NB + P::VB; b += P::TPB) mb[b] = c[b];
   supports_raw<L>(rw + P::RWW, P::W, SY);
-  fill_gf(GE, GL);
   __syncthreads();
   // u doubled: raw words = the ct's u bytes (bits >= n as received); the word straddling into v is cut
   constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
@@ -604,105 +604,180 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
     T[j] = j < P::VW32 ? acc[0][q] ^ lds_u32_unaligned(mb, P::NB + 4 * j) : 0u;
   }
   __syncthreads();
-  // duplicated RM(1,7): one wave per symbol, lane l holds positions l and l + 64
-  for (int sym = wave; sym < P::N1; sym += P::TPB / 64) {
-    const uint32_t* cw = T + sym * 4 * P::MULT;
-    int x0 = 0, x1 = 0;
+  // duplicated RM(1,7): one wave per symbol pair (two independent shuffle chains interleave),
+  // lane l holds positions l and l + 64 of each symbol
+  constexpr int NWAVE = P::TPB / 64;
+  for (int base = wave; base < P::N1; base += 2 * NWAVE) {
+    const int sy[2] = {base, base + NWAVE < P::N1 ? base + NWAVE : base};
+    int x0[2], x1[2];
 #pragma unroll
-    for (int cp = 0; cp < P::MULT; ++cp) {
-      x0 += (int)(cw[4 * cp + (lane >> 5)] >> (lane & 31) & 1);
-      x1 += (int)(cw[4 * cp + 2 + (lane >> 5)] >> (lane & 31) & 1);
-    }
-    {
-      const int a = x0, b = x1;
-      x0 = a + b;
-      x1 = a - b;
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t* cw = T + sy[u] * 4 * P::MULT;
+      x0[u] = 0;
+      x1[u] = 0;
+#pragma unroll
+      for (int cp = 0; cp < P::MULT; ++cp) {
+        x0[u] += (int)(cw[4 * cp + (lane >> 5)] >> (lane & 31) & 1);
+        x1[u] += (int)(cw[4 * cp + 2 + (lane >> 5)] >> (lane & 31) & 1);
+      }
+      const int a0 = x0[u], b0 = x1[u];
+      x0[u] = a0 + b0;
+      x1[u] = a0 - b0;
     }
 #pragma unroll
     for (int bit = 0; bit < 6; ++bit) {
-      const int p0 = __shfl_xor(x0, 1 << bit), p1 = __shfl_xor(x1, 1 << bit);
       const bool hi = (lane >> bit) & 1;
-      x0 = hi ? p0 - x0 : x0 + p0;
-      x1 = hi ? p1 - x1 : x1 + p1;
-    }
-    if (lane == 0) x0 -= 64 * P::MULT;
-    // first maximum of |value| (lowest index), sign -> bit 7
-    const uint32_t k0 = ((uint32_t)abs(x0) << 8) | ((uint32_t)(127 - lane) << 1) | (x0 > 0 ? 1u : 0u);
-    const uint32_t k1 = ((uint32_t)abs(x1) << 8) | ((uint32_t)(63 - lane) << 1) | (x1 > 0 ? 1u : 0u);
-    uint32_t k = k0 > k1 ? k0 : k1;
 #pragma unroll
-    for (int bit = 0; bit < 6; ++bit) {
-      const uint32_t o = __shfl_xor(k, 1 << bit);
-      k = o > k ? o : k;
+      for (int u = 0; u < 2; ++u) {
+        const int p0 = __shfl_xor(x0[u], 1 << bit), p1 = __shfl_xor(x1[u], 1 << bit);
+        x0[u] = hi ? p0 - x0[u] : x0[u] + p0;
+        x1[u] = hi ? p1 - x1[u] : x1[u] + p1;
+      }
     }
-    if (lane == 0) SYM[sym] = (uint8_t)((127 - ((k >> 1) & 127)) | ((k & 1) << 7));
+    uint32_t k[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (lane == 0) x0[u] -= 64 * P::MULT;
+      // first maximum of |value| (lowest index), sign -> bit 7
+      const uint32_t k0 = ((uint32_t)abs(x0[u]) << 8) | ((uint32_t)(127 - lane) << 1) | (x0[u] > 0 ? 1u : 0u);
+      const uint32_t k1 = ((uint32_t)abs(x1[u]) << 8) | ((uint32_t)(63 - lane) << 1) | (x1[u] > 0 ? 1u : 0u);
+      k[u] = k0 > k1 ? k0 : k1;
+    }
+#pragma unroll
+    for (int bit = 0; bit < 6; ++bit)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t o = __shfl_xor(k[u], 1 << bit);
+        k[u] = o > k[u] ? o : k[u];
+      }
+    if (lane == 0) {
+      SYM[sy[0]] = (uint8_t)((127 - ((k[0] >> 1) & 127)) | ((k[0] & 1) << 7));
+      SYM[sy[1]] = (uint8_t)((127 - ((k[1] >> 1) & 127)) | ((k[1] & 1) << 7));
+    }
   }
   __syncthreads();
-  if (wave != 0) return;
-  // Reed-Solomon, bounded distance: syndromes S_{i+1} = r(alpha^(i+1)), i < 2 delta
-  const Lgf gf{GE, GL};
+  if (t < P::N1) syms[hs * sym_stride + t] = SYM[t];
+}
+
+// wave-scope LDS ordering (the wave's lanes exchange through LDS)
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// XOR over the 64 lanes (all active), wave-uniform result: DPP within each 16-lane row
+// (quad swaps, half-row and row mirrors), then the four row values by v_readlane.
+__device__ __forceinline__ uint32_t xor_wave(uint32_t d) {
+  d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)(__builtin_amdgcn_readlane((int)d, 0) ^ __builtin_amdgcn_readlane((int)d, 16) ^
+                    __builtin_amdgcn_readlane((int)d, 32) ^ __builtin_amdgcn_readlane((int)d, 48));
+}
+
+// ---------------------------------------------------------------- Decaps: Reed-Solomon decoding
+// One wave per handshake, 4 per workgroup (GF(2^8) exp/log tables shared in LDS).  Bounded-distance
+// decoding as the spec: syndromes S_1..S_2delta, Berlekamp-Massey, Omega = S C mod x^(2 delta),
+// Chien search + Forney over the n1 positions; the corrected message symbols are m'.  Every sum
+// is taken in the log domain over independent table lookups (no dependent multiply chains);
+// zero is log 255.
+template <int L>
+__global__ __launch_bounds__(256) void k_hqc_rs(size_t n, const uint8_t* __restrict__ syms, size_t sym_stride,
+                                                uint8_t* __restrict__ mp) {
+  using P = HQ<L>;
+  constexpr uint32_t Z = 255;
+  __shared__ uint8_t GE[512], GL[256];
+  __shared__ uint8_t SYMW[4][128], LSW[4][128], LSYNW[4][64], CLW[4][64], LCLW[4][64], LOMW[4][64];
+  fill_gf(GE, GL);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t hs = (size_t)blockIdx.x * 4 + wave;
+  if (hs >= n) return;
+  uint8_t *SYM = SYMW[wave], *LS = LSW[wave], *LSYN = LSYNW[wave], *CL = CLW[wave], *LCL = LCLW[wave],
+          *LOM = LOMW[wave];
+  auto lg = [&](uint32_t a) { return a ? (uint32_t)GL[a] : Z; };
+  auto mod255 = [](uint32_t x) { return x >= 255 ? x - 255 : x; };
+  for (int j = lane; j < P::N1; j += 64) {
+    const uint32_t r = syms[hs * sym_stride + j];
+    SYM[j] = (uint8_t)r;
+    LS[j] = (uint8_t)lg(r);
+  }
+  wsync();
+  // syndromes S_{i+1} = sum_j r_j alpha^((i+1) j), lane i
   if (lane < P::T2) {
     uint32_t s = 0, e = 0;
     const uint32_t step = (uint32_t)(lane + 1);
+#pragma unroll 16
     for (int j = 0; j < P::N1; ++j) {
-      const uint32_t r = SYM[j];
-      const uint32_t pr = GE[GL[r] + e];
-      s ^= r ? pr : 0u;
-      e += step;
-      e = e >= 255 ? e - 255 : e;
+      const uint32_t l = LS[j];
+      s ^= l != Z ? (uint32_t)GE[l + e] : 0u;
+      e = mod255(e + step);
     }
-    SYN[lane] = (uint8_t)s;
+    LSYN[lane] = (uint8_t)lg(s);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // Berlekamp-Massey, lane j holds C_j, B_j (branch-free in the data)
-  uint32_t Cj = lane == 0 ? 1u : 0u, Bj = Cj, b = 1;
+  wsync();
+  // Berlekamp-Massey: lane j holds C_j and log B_j; the discrepancy is wave-uniform
+  uint32_t Cj = lane == 0 ? 1u : 0u, LBj = lane == 0 ? 0u : Z, lb = 0;
   int Lr = 0, m = 1;
   for (int i = 0; i < P::T2; ++i) {
-    const uint32_t term = (lane <= Lr && lane <= i) ? gf.mul(Cj, SYN[i - (lane <= i ? lane : 0)]) : 0u;
-    uint32_t d = term;
-#pragma unroll
-    for (int bit = 0; bit < 6; ++bit) d ^= __shfl_xor(d, 1 << bit);
-    const uint32_t coef = gf.mul(d, gf.inv(b));
-    const uint32_t bsh = __shfl(Bj, lane - m >= 0 ? lane - m : 0);
-    const uint32_t cn = Cj ^ (lane >= m ? gf.mul(coef, bsh) : 0u);
-    const bool upd = d != 0 && 2 * Lr <= i;
-    Bj = upd ? Cj : Bj;
-    b = upd ? d : b;
-    Lr = upd ? i + 1 - Lr : Lr;
-    m = upd ? 1 : m + 1;
-    Cj = cn;
+    const uint32_t lbsh = (uint32_t)__shfl((int)LBj, lane - m >= 0 ? lane - m : 0);
+    const uint32_t lc = lg(Cj);
+    const uint32_t ls = lane <= i ? (uint32_t)LSYN[i - lane] : Z;
+    const uint32_t term = (lane <= Lr && lc != Z && ls != Z) ? (uint32_t)GE[lc + ls] : 0u;
+    const uint32_t d = xor_wave(term);
+    if (d != 0) {
+      const uint32_t ld = GL[d];
+      const uint32_t lcoef = mod255(ld + 255 - lb);
+      const uint32_t cn = Cj ^ ((lane >= m && lbsh != Z) ? (uint32_t)GE[lcoef + lbsh] : 0u);
+      if (2 * Lr <= i) {
+        LBj = lc;
+        lb = ld;
+        Lr = i + 1 - Lr;
+        m = 1;
+      } else {
+        ++m;
+      }
+      Cj = cn;
+    } else {
+      ++m;
+    }
   }
-  if (lane <= P::T2) CL[lane] = (uint8_t)Cj;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // Omega = S(x) C(x) mod x^(2 delta)
+  if (lane <= P::T2) {
+    CL[lane] = (uint8_t)Cj;
+    LCL[lane] = (uint8_t)lg(Cj);
+  }
+  wsync();
+  // Omega_i = sum_{j <= i} S_{i-j+1} C_j, i < 2 delta
   if (lane < P::T2) {
     uint32_t o = 0;
-    for (int j = 0; j <= lane; ++j) o ^= gf.mul(SYN[lane - j], CL[j]);
-    OM[lane] = (uint8_t)o;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // Chien search + Forney over the n1 positions
-  for (int pos = lane; pos < P::N1; pos += 64) {
-    const uint32_t lx = (uint32_t)((255 - pos) % 255);  // log of alpha^(-pos)
-    auto mulx = [&](uint32_t a) { return a ? (uint32_t)GE[GL[a] + lx] : 0u; };
-    uint32_t cv = 0, dv = 0, ov = 0;
-    for (int i = P::T2; i >= 0; --i) cv = mulx(cv) ^ CL[i];
-    for (int i = P::T2 - 1; i >= 0; --i) {
-      dv = mulx(dv) ^ ((i & 1) == 0 ? CL[i + 1] : 0u);
-      ov = mulx(ov) ^ OM[i];
+#pragma unroll 8
+    for (int j = 0; j < P::T2; ++j) {
+      const uint32_t ls = j <= lane ? (uint32_t)LSYN[lane - j] : Z, lc = LCL[j];
+      o ^= (ls != Z && lc != Z) ? (uint32_t)GE[ls + lc] : 0u;
     }
-    const uint32_t fix = (cv == 0 && dv != 0) ? gf.mul(ov, gf.inv(dv)) : 0u;
+    LOM[lane] = (uint8_t)lg(o);
+  }
+  wsync();
+  // Chien search + Forney, lane per position: x = alpha^(-pos);
+  // C(x), C'(x) = sum_{i even} C_{i+1} x^i, Omega(x); error value Omega(x) / C'(x) where C(x) = 0
+  for (int pos = lane; pos < P::N1; pos += 64) {
+    const uint32_t lx = (uint32_t)((255 - pos) % 255);
+    uint32_t cv = CL[0], dv = 0, ov = 0, e = 0;  // e = log x^i
+#pragma unroll 8
+    for (int i = 0; i < P::T2; ++i) {
+      const uint32_t lo = LOM[i], ld = (i & 1) == 0 ? (uint32_t)LCL[i + 1] : Z, lc1 = LCL[i + 1];
+      const uint32_t e1 = mod255(e + lx);  // log x^(i+1)
+      ov ^= lo != Z ? (uint32_t)GE[lo + e] : 0u;
+      dv ^= ld != Z ? (uint32_t)GE[ld + e] : 0u;
+      cv ^= lc1 != Z ? (uint32_t)GE[lc1 + e1] : 0u;
+      e = e1;
+    }
+    const uint32_t fix = (cv == 0 && dv != 0 && ov != 0) ? (uint32_t)GE[GL[ov] + 255 - GL[dv]] : 0u;
     SYM[pos] ^= (uint8_t)fix;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wsync();
   if (lane < P::K) mp[hs * 32 + lane] = SYM[P::T2 + lane];
 }
 
@@ -790,7 +865,12 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   View v = carve<L>(scratch, n);
   int32_t* stp = status ? status : v.st;
   QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.row);
-  QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, ct, v.mp);
+  // the RM stage's symbols go through the K-hash message area, which is free until the re-encryption
+  uint8_t* syms = (uint8_t*)v.msg;
+  QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, ct, syms,
+             (size_t)P::MW * 8);
+  QRK_LAUNCH("k_hqc_rs", st, k_hqc_rs<L>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n, (const uint8_t*)syms,
+             (size_t)P::MW * 8, v.mp);
   QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.mp, (size_t)32,
              sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row);
   QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row,
