@@ -33,7 +33,9 @@ namespace hqc {
 constexpr int SEED = 40, SALT = 16, SSB = 64;
 
 // TPB threads per handshake in the workgroup kernels, WPT output words per thread (odd, so a
-// wave's contiguous WPT+1-word windows fall on distinct LDS banks)
+// wave's contiguous WPT+1-word windows fall on distinct LDS banks).  Tried: 64-bit windows
+// (WPT = 6, ds_read_b64, fewer threads per product) -- slower: the products are latency-bound,
+// not LDS-bandwidth-bound (profiles/r1/sq_hqc128_b16.txt)
 template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_, int TPB_>
 struct Params {
   static constexpr int N = N_, N1 = N1_, N2 = N2_, W = W_, WR = WR_, WE = WE_, K = K_, DELTA = DELTA_,
@@ -148,6 +150,19 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {
   const uint32_t w0 = b[0], w1 = b[1];
   const uint32_t w2 = sh ? b[2] : 0u;
   return (uint64_t)alignbit(w1, w0, sh) | ((uint64_t)alignbit(w2, w1, sh) << 32);
+}
+
+// word j (little-endian) of the nbytes-long byte string at src (any alignment), bytes past the
+// end read as 0: one or two aligned dword loads, each holding at least one byte of the string
+__device__ __forceinline__ uint32_t ld32_masked(const uint8_t* src, int j, int nbytes) {
+  const uintptr_t a = (uintptr_t)src + 4 * (uintptr_t)j;
+  const uint32_t* b = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  const int valid = nbytes - 4 * j;  // >= 1
+  const uint32_t w0 = b[0];
+  const uint32_t w1 = (sh != 0 && valid > 4 - (int)(sh >> 3)) ? b[1] : 0u;
+  const uint32_t w = sh ? alignbit(w1, w0, sh) : w0;
+  return valid >= 4 ? w : (w & ((1u << (8 * valid)) - 1));
 }
 
 // one-block SHAKE256 over NWM words that already hold the message, domain byte and 0x1F pad
@@ -352,6 +367,7 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
     const uint32_t v = rd(j);
     return j == P::NW32 - 1 ? (v & TOPMASK) : v;
   };
+#pragma unroll 4
   for (int q = threadIdx.x; q < P::NH2; q += P::TPB) {
     uint32_t v = q < P::NW32 ? rd(q) : 0u;
     if (q >= P::N32) v ^= alignbit(clean(q - P::N32), clean(q - P::N32 - 1), 32 - P::NR);
@@ -365,7 +381,9 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
                                              uint32_t (&acc)[NV][HQ<L>::WPT]) {
   using P = HQ<L>;
   const int j0 = threadIdx.x * P::WPT;
-#pragma unroll 1
+  // unrolled so the next positions' support reads and operand windows are in flight together
+  // (one position per iteration is a chain of two dependent LDS round trips)
+#pragma unroll 4
   for (int i = 0; i < weight; ++i) {
     const uint32_t k = sup[i];
     const uint32_t e = (uint32_t)P::N - k;
@@ -432,7 +450,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   supports_raw<L>(rw, P::W, SX);
   supports_raw<L>(rw + P::RWW, P::W, SY);
   // sk = sk_seed || sigma || pk_seed || s  (the coins' first 80 + K bytes, in order)
-  for (int b = t; b < P::KPC; b += P::TPB) mb[b] = c[b];
+  for (int j = t; j < (P::KPC + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::KPC);
   __syncthreads();
   dedupe_wg<L, 2, P::W>(SS, PJ);
   uint32_t acc[1][P::WPT] = {};
@@ -450,7 +468,9 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   __syncthreads();
   uint8_t* so = sk + hs * P::SK;
   uint8_t* po = pk + hs * P::PK;
+#pragma unroll 8
   for (int b = t; b < P::SK; b += P::TPB) so[b] = mb[b];
+#pragma unroll 8
   for (int b = t; b < P::PK; b += P::TPB) po[b] = mb[SEED + P::K + b];
 }
 
@@ -483,7 +503,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   // phase A: h doubled, s staged (bytes), supports, m, GF tables
   const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });
-  for (int b = t; b < 4 * P::NW32; b += P::TPB) mb[b] = b < P::NB ? spk[SEED + b] : 0;
+  for (int j = t; j < P::NW32; j += P::TPB) MB[j] = ld32_masked(spk + SEED, j, P::NB);
   supports_raw<L>(rw, P::WR, S1);
   supports_raw<L>(rw + P::RWR, P::WR, S2);
   supports_raw<L>(rw + 2 * P::RWR, P::WE, SE);
@@ -497,6 +517,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
     const RsTab<L>& rs = rs_tab<L>();
     if (lane < P::T2) {
       uint32_t par = 0;
+#pragma unroll
       for (int i = 0; i < P::K; ++i) {
         const uint32_t mi = MM[i], lp = rs.lp[i][lane];
         const uint32_t pr = GE[GL[mi] + lp];
@@ -535,7 +556,8 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   } else {
     // received u || v into the message area, then compare with the re-encryption
     const uint8_t* cin = ct_in + hs * P::CT;
-    for (int b = t; b < P::NB + P::VB; b += P::TPB) mb[P::K + b] = cin[b];
+    static_assert(P::K % 4 == 0, "u || v starts on a word");
+    for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[P::K / 4 + j] = ld32_masked(cin, j, P::NB + P::VB);
     __syncthreads();
     uint32_t diff = 0;
     for (int j = t; j < P::NW32; j += P::TPB) {
@@ -563,6 +585,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   for (int w = t; w < P::MW; w += P::TPB) mo[w] = m64[w];
   if constexpr (!REENC) {
     uint8_t* co = ct_out + hs * P::CT;
+#pragma unroll 8
     for (int b = t; b < P::NB + P::VB; b += P::TPB) co[b] = mb[P::K + b];
     if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
   }
@@ -585,8 +608,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   const uint64_t* rw = row + hs * P::ROWW;
   uint8_t* mb = (uint8_t*)MB;
   const uint8_t* c = ct + hs * P::CT;
-  for (int b = t; b < 4 * P::NW32; b += P::TPB) mb[b] = b < P::NB + P::VB ? c[b] : 0;
-  for (int b = 4 * P::NW32 + t; b < P::NB + P::VB; b += P::TPB) mb[b] = c[b];
+  for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::NB + P::VB);
   supports_raw<L>(rw + P::RWW, P::W, SY);
   __syncthreads();
   // u doubled: raw words = the ct's u bytes (bits >= n as received); the word straddling into v is cut
