@@ -591,6 +591,52 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   }
 }
 
+// Hadamard butterfly on lane bit BIT for two symbols (x0 / x1 = positions l / l + 64):
+// x = hi ? partner - x : x + partner, partner = the value of lane l ^ (1 << BIT).
+// Partners without LDS: quad_perm DPP (bits 0, 1), row_shl/row_shr:4 under bank masks (bit 2),
+// row_ror:8 (bit 3), v_permlane16_swap / v_permlane32_swap (bits 4, 5).  All lanes active.
+template <int BIT>
+__device__ __forceinline__ int lane_partner(int x, int lane) {
+  if constexpr (BIT == 0) {
+    return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (BIT == 1) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (BIT == 2) {
+    const int p = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xF, 0x5, false);  // banks 0, 2: lane + 4
+    return __builtin_amdgcn_update_dpp(p, x, 0x114, 0xF, 0xA, false);         // banks 1, 3: lane - 4
+  } else if constexpr (BIT == 3) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (BIT == 4) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+    return (int)(((lane >> 4) & 1) ? r[0] : r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+    return (int)((lane >> 5) ? r[0] : r[1]);
+  }
+}
+template <int BIT>
+__device__ __forceinline__ void butterflies(int (&x0)[2], int (&x1)[2], int lane) {
+  const bool hi = (lane >> BIT) & 1;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p0 = lane_partner<BIT>(x0[u], lane), p1 = lane_partner<BIT>(x1[u], lane);
+    x0[u] = hi ? p0 - x0[u] : x0[u] + p0;
+    x1[u] = hi ? p1 - x1[u] : x1[u] + p1;
+  }
+}
+// wave-uniform maximum (all lanes active): DPP within rows, then the four rows by v_readlane
+__device__ __forceinline__ uint32_t max_wave(uint32_t k) {
+  auto mx = [](uint32_t a, int b) { return a > (uint32_t)b ? a : (uint32_t)b; };
+  k = mx(k, __builtin_amdgcn_update_dpp(0, (int)k, 0xB1, 0xF, 0xF, false));
+  k = mx(k, __builtin_amdgcn_update_dpp(0, (int)k, 0x4E, 0xF, 0xF, false));
+  k = mx(k, __builtin_amdgcn_update_dpp(0, (int)k, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  k = mx(k, __builtin_amdgcn_update_dpp(0, (int)k, 0x140, 0xF, 0xF, false));  // row_mirror
+  const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)k, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)k, 16);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)k, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)k, 48);
+  const uint32_t ab = a > b ? a : b, cd = c > d ? c : d;
+  return ab > cd ? ab : cd;
+}
+
 // ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
 template <int L>
 __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
@@ -626,8 +672,9 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
     T[j] = j < P::VW32 ? acc[0][q] ^ lds_u32_unaligned(mb, P::NB + 4 * j) : 0u;
   }
   __syncthreads();
-  // duplicated RM(1,7): one wave per symbol pair (two independent shuffle chains interleave),
-  // lane l holds positions l and l + 64 of each symbol
+  // duplicated RM(1,7): one wave per symbol pair (two independent chains interleave), lane l
+  // holds positions l and l + 64 of each symbol; the Hadamard butterflies exchange through DPP
+  // and v_permlane16/32_swap (no LDS round trips), the first maximum is a DPP + readlane max
   constexpr int NWAVE = P::TPB / 64;
   for (int base = wave; base < P::N1; base += 2 * NWAVE) {
     const int sy[2] = {base, base + NWAVE < P::N1 ? base + NWAVE : base};
@@ -646,35 +693,20 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
       x0[u] = a0 + b0;
       x1[u] = a0 - b0;
     }
-#pragma unroll
-    for (int bit = 0; bit < 6; ++bit) {
-      const bool hi = (lane >> bit) & 1;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int p0 = __shfl_xor(x0[u], 1 << bit), p1 = __shfl_xor(x1[u], 1 << bit);
-        x0[u] = hi ? p0 - x0[u] : x0[u] + p0;
-        x1[u] = hi ? p1 - x1[u] : x1[u] + p1;
-      }
-    }
-    uint32_t k[2];
+    butterflies<0>(x0, x1, lane);
+    butterflies<1>(x0, x1, lane);
+    butterflies<2>(x0, x1, lane);
+    butterflies<3>(x0, x1, lane);
+    butterflies<4>(x0, x1, lane);
+    butterflies<5>(x0, x1, lane);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (lane == 0) x0[u] -= 64 * P::MULT;
       // first maximum of |value| (lowest index), sign -> bit 7
       const uint32_t k0 = ((uint32_t)abs(x0[u]) << 8) | ((uint32_t)(127 - lane) << 1) | (x0[u] > 0 ? 1u : 0u);
       const uint32_t k1 = ((uint32_t)abs(x1[u]) << 8) | ((uint32_t)(63 - lane) << 1) | (x1[u] > 0 ? 1u : 0u);
-      k[u] = k0 > k1 ? k0 : k1;
-    }
-#pragma unroll
-    for (int bit = 0; bit < 6; ++bit)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const uint32_t o = __shfl_xor(k[u], 1 << bit);
-        k[u] = o > k[u] ? o : k[u];
-      }
-    if (lane == 0) {
-      SYM[sy[0]] = (uint8_t)((127 - ((k[0] >> 1) & 127)) | ((k[0] & 1) << 7));
-      SYM[sy[1]] = (uint8_t)((127 - ((k[1] >> 1) & 127)) | ((k[1] & 1) << 7));
+      const uint32_t k = max_wave(k0 > k1 ? k0 : k1);
+      if (lane == 0) SYM[sy[u]] = (uint8_t)((127 - ((k >> 1) & 127)) | ((k & 1) << 7));
     }
   }
   __syncthreads();
