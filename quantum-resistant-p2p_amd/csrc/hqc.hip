@@ -32,20 +32,24 @@ namespace hqc {
 
 constexpr int SEED = 40, SALT = 16, SSB = 64;
 
-// TPB threads per handshake in the workgroup kernels, WPT output words per thread (odd, so a
-// wave's contiguous WPT+1-word windows fall on distinct LDS banks).  Tried: 64-bit windows
-// (WPT = 6, ds_read_b64, fewer threads per product) -- slower: the products are latency-bound,
-// not LDS-bandwidth-bound (profiles/r1/sq_hqc128_b16.txt)
-template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_, int TPB_>
+// TPB threads per handshake in the workgroup kernels.  In the sparse-dense products the threads
+// form PC = TPB / NBT position classes of NBT threads: thread t owns WPT consecutive output
+// words (j0 = (t % NBT) * WPT) and the positions i = t / NBT (mod PC); the classes' partial sums
+// are XOR-combined in LDS.  Fewer, longer per-position windows (WPT + 1 reads for WPT words) and
+// a position chain PC times shorter per wave: the products are latency-bound
+// (profiles/r1/sq_hqc128_b16.txt).  WPT odd, so a wave's windows fall on distinct LDS banks.
+// (WPT, NBT): one-operand products (KeyGen, Decaps); (WPTE, NBTE): Encaps' two-operand product.
+template <int N_, int N1_, int N2_, int W_, int WR_, int WE_, int K_, int DELTA_, int MULT_, int WPT_, int NBT_,
+          int WPTE_, int NBTE_, int TPB_>
 struct Params {
   static constexpr int N = N_, N1 = N1_, N2 = N2_, W = W_, WR = WR_, WE = WE_, K = K_, DELTA = DELTA_,
-                       MULT = MULT_, WPT = WPT_, TPB = TPB_;
+                       MULT = MULT_, WPT = WPT_, NBT = NBT_, WPTE = WPTE_, NBTE = NBTE_, TPB = TPB_;
   static constexpr int NB = (N + 7) / 8, VB = N1 * N2 / 8;
   static constexpr int NW32 = (N + 31) / 32, VW32 = VB / 4, N32 = N >> 5, NR = N & 31;
   static constexpr int NHW = (NB + 7) / 8;  // h stream words (the seedexpander squeezes 8-byte units)
   static constexpr int PK = SEED + NB, SK = SEED + K + PK, CT = NB + VB + SALT, KPC = 2 * SEED + K, ENC = K + SALT;
   static constexpr int RWW = (4 * W + 7) / 8, RWR = (4 * WR + 7) / 8, RWE = (4 * WE + 7) / 8;
-  static constexpr int NWP = TPB * WPT, NH2 = NWP + N32 + 2;
+  static constexpr int NWP = NBT * WPT > NBTE * WPTE ? NBT * WPT : NBTE * WPTE, NH2 = NWP + N32 + 2;
   static constexpr int MSGB = K + NB + VB, MW = (MSGB + 2 + 7) / 8;  // K-hash message || 0x05 || 0x1F, words
   static constexpr int MBW = ((SK > 8 * MW ? SK : 8 * MW) + 15) / 4;  // LDS byte buffer, words
   static constexpr int T2 = 2 * DELTA, WMAX = W > WR ? W : WR;
@@ -53,13 +57,17 @@ struct Params {
   static constexpr int ROWW = ROW_ENC > ROW_KG ? ROW_ENC : ROW_KG;
   static_assert(NR != 0, "n is never a multiple of 32 for HQC");
   static_assert(T2 + 1 <= 64 && WMAX <= 192 && N1 <= 128, "lane mappings");
-  static_assert(NWP >= NW32, "WPT too small");
-  static_assert(WPT % 2 == 1 && TPB % 64 == 0 && TPB >= 256, "bank-conflict-free windows; >= 4 waves");
+  static_assert(NBT * WPT >= NW32 && NBTE * WPTE >= NW32, "WPT too small");
+  static_assert(WPT % 2 == 1 && NBT % 64 == 0 && TPB % NBT == 0 && WPTE % 2 == 1 && NBTE % 64 == 0 &&
+                    TPB % NBTE == 0 && TPB >= 256,
+                "bank-conflict-free windows; whole waves per position class; >= 4 waves");
 };
 template <int L> struct HQ;
-template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 3, 256> {};
-template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 5, 256> {};
-template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 5, 384> {};
+// A/B on one box (2^16): HQC-128 (5, 128) for both beats (9, 64) + (5, 256); HQC-256 Encaps keeps
+// one position class (5, 384) while its Decaps gains from three (15, 128) (profiles/r1/ab_hqc_prod.txt)
+template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 5, 128, 5, 128, 256> {};
+template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 5, 256, 256> {};
+template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 384, 384> {};
 
 // ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
 struct GfTabs {
@@ -375,29 +383,54 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   }
 }
 
-// acc[c] ^= word (j0 + c) of X^k D-operand, for every position k of sup
-template <int L, int NV>
+// acc[c] ^= word (j0 + c) of X^k D-operand for the positions k of sup in this thread's class
+// (partial sums; prod_combine adds the classes)
+template <int L, int NV, int WPT, int NBT>
 __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, const uint32_t* const (&D)[NV],
-                                             uint32_t (&acc)[NV][HQ<L>::WPT]) {
+                                             uint32_t (&acc)[NV][WPT]) {
   using P = HQ<L>;
-  const int j0 = threadIdx.x * P::WPT;
-  // unrolled so the next positions' support reads and operand windows are in flight together
-  // (one position per iteration is a chain of two dependent LDS round trips)
-#pragma unroll 4
-  for (int i = 0; i < weight; ++i) {
+  constexpr int PC = P::TPB / NBT;
+  const int j0 = (int)(threadIdx.x % NBT) * WPT;
+  // one operand: unrolled so the next position's support read and window are in flight together;
+  // two operands: not unrolled (both windows already in flight; keeps <= 64 VGPRs, 8 waves / SIMD)
+  constexpr int UNR = NV == 1 ? 2 : 1;
+#pragma unroll UNR
+  for (int i = (int)(threadIdx.x / NBT); i < weight; i += PC) {
     const uint32_t k = sup[i];
     const uint32_t e = (uint32_t)P::N - k;
     const int off = (int)(e >> 5) + j0;
     const uint32_t sh = e & 31;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      uint32_t w[P::WPT + 1];
+      uint32_t w[WPT + 1];
 #pragma unroll
-      for (int c = 0; c <= P::WPT; ++c) w[c] = D[v][off + c];
+      for (int c = 0; c <= WPT; ++c) w[c] = D[v][off + c];
 #pragma unroll
-      for (int c = 0; c < P::WPT; ++c) acc[v][c] ^= alignbit(w[c + 1], w[c], sh);
+      for (int c = 0; c < WPT; ++c) acc[v][c] ^= alignbit(w[c + 1], w[c], sh);
     }
   }
+}
+
+// out[v][j0 + c] = the product words: class 0 stores, the other classes XOR in after a barrier.
+// Call with the operands no longer needed by any thread (out may alias them); `extra` runs in the
+// XOR phase (further commutative updates of out).  Ends with a barrier.
+template <int NV, int WPT, int NBT, typename Extra>
+__device__ __forceinline__ void prod_combine(uint32_t* const (&out)[NV], const uint32_t (&acc)[NV][WPT], Extra extra) {
+  const int j0 = (int)(threadIdx.x % NBT) * WPT;
+  const bool first = threadIdx.x < NBT;
+  if (first)
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int q = 0; q < WPT; ++q) out[v][j0 + q] = acc[v][q];
+  __syncthreads();
+  if (!first)
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int q = 0; q < WPT; ++q) atomicXor(&out[v][j0 + q], acc[v][q]);
+  extra();
+  __syncthreads();
 }
 
 // RM(1,7) codeword word q (0..3) of symbol b: bit j = b7 ^ <b0..6, j>
@@ -455,14 +488,12 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   dedupe_wg<L, 2, P::W>(SS, PJ);
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D};
-  sparse_dense<L, 1>(SY, P::W, Ds, acc);
+  sparse_dense<L, 1, P::WPT, P::NBT>(SY, P::W, Ds, acc);
   __syncthreads();  // D is reused as the output buffer
-  const int j0 = t * P::WPT;
-#pragma unroll
-  for (int q = 0; q < P::WPT; ++q) D[j0 + q] = acc[0][q];
-  __syncthreads();
-  for (int i = t; i < P::W; i += P::TPB) atomicXor(&D[SX[i] >> 5], 1u << (SX[i] & 31));
-  __syncthreads();
+  uint32_t* const outs[1] = {D};
+  prod_combine<1, P::WPT, P::NBT>(outs, acc, [&] {
+    for (int i = t; i < P::W; i += P::TPB) atomicXor(&D[SX[i] >> 5], 1u << (SX[i] & 31));
+  });
   constexpr int SOFF = (2 * SEED + P::K) / 4;  // s at byte 80 + K (a multiple of 4)
   for (int j = t; j < P::NW32; j += P::TPB) MB[SOFF + j] = j == P::NW32 - 1 ? (D[j] & ((1u << P::NR) - 1)) : D[j];
   __syncthreads();
@@ -531,17 +562,15 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   }
   dedupe_wg<L, 3, P::WR>(SS, PJ);  // ends with a barrier
   // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
-  uint32_t acc[2][P::WPT] = {};
+  uint32_t acc[2][P::WPTE] = {};
   const uint32_t* const Ds[2] = {D1, D2};
-  sparse_dense<L, 2>(S2, P::WR, Ds, acc);
+  sparse_dense<L, 2, P::WPTE, P::NBTE>(S2, P::WR, Ds, acc);
   __syncthreads();
-  const int j0 = t * P::WPT;
-#pragma unroll
-  for (int q = 0; q < P::WPT; ++q) D1[j0 + q] = acc[0][q], D2[j0 + q] = acc[1][q];
-  __syncthreads();
-  for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
-  for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
-  __syncthreads();
+  uint32_t* const outs[2] = {D1, D2};
+  prod_combine<2, P::WPTE, P::NBTE>(outs, acc, [&] {
+    for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
+    for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
+  });
   constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
   constexpr int UOFF = P::K / 4;  // u at message byte K
   auto vword = [&](int j) {       // v word j = (r2 s + e + codeword) word j
@@ -664,14 +693,22 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   dedupe_wg<L, 1, P::W>(SY, PJ);
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D1};
-  sparse_dense<L, 1>(SY, P::W, Ds, acc);
-  const int j0 = t * P::WPT;
+  sparse_dense<L, 1, P::WPT, P::NBT>(SY, P::W, Ds, acc);
+  // T = v - u y (words >= VW32 zero): fold v into class 0's partial sums, then combine
+  if (t < P::NBT) {
+    const int j0 = t * P::WPT;
 #pragma unroll
-  for (int q = 0; q < P::WPT; ++q) {
-    const int j = j0 + q;
-    T[j] = j < P::VW32 ? acc[0][q] ^ lds_u32_unaligned(mb, P::NB + 4 * j) : 0u;
+    for (int q = 0; q < P::WPT; ++q) {
+      const int j = j0 + q;
+      acc[0][q] = j < P::VW32 ? acc[0][q] ^ lds_u32_unaligned(mb, P::NB + 4 * j) : 0u;
+    }
+  } else {
+    const int j0 = (t % P::NBT) * P::WPT;
+#pragma unroll
+    for (int q = 0; q < P::WPT; ++q) acc[0][q] = j0 + q < P::VW32 ? acc[0][q] : 0u;
   }
-  __syncthreads();
+  uint32_t* const outs[1] = {T};
+  prod_combine<1, P::WPT, P::NBT>(outs, acc, [] {});
   // duplicated RM(1,7): one wave per symbol pair (two independent chains interleave), lane l
   // holds positions l and l + 64 of each symbol; the Hadamard butterflies exchange through DPP
   // and v_permlane16/32_swap (no LDS round trips), the first maximum is a DPP + readlane max
