@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Issued VALU op rate per kernel from a tools/pmc_sq.sh pass, against the gfx950 peak.
+
+    tools/valu_rate.py gpurun_out/sq_<tag> <bench line .json> <out.json>
+
+SQ_INSTS_VALU (wave instructions per dispatch, pass "a") x 64 lanes = issued 32-bit lane-ops;
+divided by the kernel's isolated average duration from the bench line's "kernels" object (the
+serial profiled step: rocprofv3 serialises dispatches while it collects counters, so the
+isolated duration is the matching one).  Reported against the nominal 78.6 T lane-ops/s
+(256 CU x 4 SIMD x 32 lanes x 2.4 GHz, bench.py VALU_PEAK) and the measured full-rate issue
+ceiling (v_xor / v_add / v_bitop3 microbenchmark, profiles/r1/valu_peak_r1b.json).  Half-rate
+instructions (v_alignbit, v_perm, VOP3 and/or/lshl_or, 24-bit multiplies) count once here but
+occupy two issue slots, so issued/peak understates how busy the VALU is; the bench line's
+algorithmic rate ("achieved_Tops") divided by the issued rate gives the fraction of issued
+instructions that the algorithmic count covers.
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+PEAK = 78.6432  # T lane-ops/s
+FULL_RATE = 61.26  # v_xor_b32 measured, T lane-ops/s
+
+
+def bench_name(pmc_name: str) -> str:
+    base = pmc_name.split("<")[0]
+    if base == "k_xof" and "true" in pmc_name:
+        return "k_xof_fix"
+    return base
+
+
+def main() -> None:
+    d, bench_path, out = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
+    bench = json.loads(bench_path.read_text().strip().splitlines()[-1])
+    kernels = bench.get("kernels") or {}
+    acc = defaultdict(lambda: defaultdict(float))
+    cnt = defaultdict(lambda: defaultdict(int))
+    for sub in ("a", "b"):
+        p = d / sub / "run_counter_collection.csv"
+        if not p.exists():
+            continue
+        for row in csv.DictReader(open(p)):
+            m = re.search(r"(k_\w+)(<[^(]*>)?\(", row["Kernel_Name"])
+            if not m:
+                continue
+            k = m.group(1) + (m.group(2) or "")
+            acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            cnt[k][row["Counter_Name"]] += 1
+    res = {}
+    for k, c in acc.items():
+        n = {x: c[x] / max(cnt[k][x], 1) for x in c}
+        b = kernels.get(bench_name(k))
+        if not b or "SQ_INSTS_VALU" not in n:
+            continue
+        t = b["avg_ms"] * 1e-3
+        issued = n["SQ_INSTS_VALU"] * 64 / t / 1e12
+        r = {"valu_wave_instrs_per_dispatch": n["SQ_INSTS_VALU"], "lds_instrs_per_dispatch": n.get("SQ_INSTS_LDS"),
+             "avg_ms_isolated": b["avg_ms"], "issued_Tops": issued, "issued_frac_of_peak": issued / PEAK,
+             "issued_frac_of_full_rate_ceiling": issued / FULL_RATE}
+        if n.get("SQ_WAVE_CYCLES"):
+            r["wave_cycles_valu_active"] = n.get("SQ_ACTIVE_INST_VALU", 0) / n["SQ_WAVE_CYCLES"]
+            r["wave_cycles_waiting"] = n.get("SQ_WAIT_ANY", 0) / n["SQ_WAVE_CYCLES"]
+        if b.get("achieved_Tops"):
+            r["algorithmic_Tops"] = b["achieved_Tops"]
+            r["algorithmic_over_issued"] = b["achieved_Tops"] / issued
+        res[k] = r
+    summary = {"source": str(d), "bench": str(bench_path), "peak_Tops": PEAK, "full_rate_ceiling_Tops": FULL_RATE,
+               "kernels": res}
+    out.write_text(json.dumps(summary, indent=1) + "\n")
+    for k, r in sorted(res.items(), key=lambda kv: -kv[1]["avg_ms_isolated"]):
+        print(f"{k[:34]:34s} {r['avg_ms_isolated']:7.3f} ms  issued {r['issued_Tops']:5.1f} Tops "
+              f"= {r['issued_frac_of_peak']:.2f} of peak, {r['issued_frac_of_full_rate_ceiling']:.2f} of full-rate"
+              + (f"  alg/issued {r['algorithmic_over_issued']:.2f}" if "algorithmic_over_issued" in r else ""))
+
+
+if __name__ == "__main__":
+    main()
