@@ -36,6 +36,7 @@ PERM_OPS = 4320  # VALU ops per Keccak-f[1600] on gfx950 (180 per round x 24, on
 # Peak int32 VALU lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md:
 # 4 SIMD-32 per CU; 157.3 TF FP32 vector = this rate x 2 flop/FMA).
 VALU_PEAK = 256 * 4 * 32 * 2.4e9
+VALU_FULL_RATE = 61.26  # T lane-ops/s: measured v_xor_b32 issue ceiling (profiles/r1/valu_peak_r1b.json)
 KP = {"ML-KEM-512": (2, 3, 2, 10, 4), "ML-KEM-768": (3, 2, 2, 10, 4), "ML-KEM-1024": (4, 2, 2, 11, 5)}
 
 
@@ -267,6 +268,21 @@ def pmc_traffic(alg, mode, chunk, kernel):
     if not e:
         return None, None
     for k, v in e["hbm_bytes_per_dispatch"].items():
+        if k == kernel or k.startswith(kernel + "<") and "true" not in k:
+            return v, e["source"]
+    return None, None
+
+
+def pmc_issued(alg, mode, chunk, kernel):
+    """Issued VALU lane-ops/s (T) of `kernel` in isolation from the committed SQ_INSTS_VALU pass
+    of the same configuration (profiles/valu_rate.json, written by tools/valu_rate.py), or None."""
+    idx = ROOT / "profiles" / "valu_rate.json"
+    if not idx.exists():
+        return None, None
+    e = json.loads(idx.read_text()).get(f"{alg}|{mode}|{chunk}")
+    if not e:
+        return None, None
+    for k, v in e["issued_Tops"].items():
         if k == kernel or k.startswith(kernel + "<") and "true" not in k:
             return v, e["source"]
     return None, None
@@ -746,6 +762,11 @@ def main():
         roof["traffic_source"] = src
         roof["algorithmic_ops_per_launch"] = roof.pop("ops_per_launch")
         roof["isolated_frac"] = roof_iso["frac"] if roof_iso and roof_iso["kernel"] == roof["kernel"] else None
+        iss, iss_src = pmc_issued(alg, args.mode, chunk_eff, roof["kernel"])
+        if roof["bound"] == "valu" and iss:
+            # every issued VALU instruction x 64 lanes over the isolated kernel time (rocprofv3 PMC)
+            roof["issued"] = {"Tops": iss, "frac": iss * 1e12 / VALU_PEAK, "full_rate_ceiling_Tops": VALU_FULL_RATE,
+                              "frac_of_full_rate_ceiling": iss / VALU_FULL_RATE, "source": iss_src}
         kp = keccak_practical_peak()
         if roof["bound"] == "valu" and kp:
             # the measured ceiling of the Keccak instruction mix (half-rate v_alignbit), see DESIGN.md 7

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Issued VALU op rate per kernel from a tools/pmc_sq.sh pass, against the gfx950 peak.
 
-    tools/valu_rate.py gpurun_out/sq_<tag> <bench line .json> <out.json>
+    tools/valu_rate.py gpurun_out/sq_<tag> <bench line .json> <out.json> [<alg|mode|chunk> key]
+
+With a key, the per-kernel issued rates are also recorded in profiles/valu_rate.json, which
+bench.py reads to add roofline.issued for the same configuration.
 
 SQ_INSTS_VALU (wave instructions per dispatch, pass "a") x 64 lanes = issued 32-bit lane-ops;
 divided by the kernel's isolated average duration from the bench line's "kernels" object (the
@@ -70,6 +73,12 @@ def main() -> None:
     summary = {"source": str(d), "bench": str(bench_path), "peak_Tops": PEAK, "full_rate_ceiling_Tops": FULL_RATE,
                "kernels": res}
     out.write_text(json.dumps(summary, indent=1) + "\n")
+    if len(sys.argv) > 4:
+        idx = Path(__file__).resolve().parent.parent / "profiles" / "valu_rate.json"
+        all_ = json.loads(idx.read_text()) if idx.exists() else {}
+        all_[sys.argv[4]] = {"issued_Tops": {k: r["issued_Tops"] for k, r in res.items()},
+                             "source": str(out)}
+        idx.write_text(json.dumps(all_, indent=1, sort_keys=True) + "\n")
     for k, r in sorted(res.items(), key=lambda kv: -kv[1]["avg_ms_isolated"]):
         print(f"{k[:34]:34s} {r['avg_ms_isolated']:7.3f} ms  issued {r['issued_Tops']:5.1f} Tops "
               f"= {r['issued_frac_of_peak']:.2f} of peak, {r['issued_frac_of_full_rate_ceiling']:.2f} of full-rate"
