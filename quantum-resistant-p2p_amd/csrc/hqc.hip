@@ -6,7 +6,7 @@
 //
 // Kernels (C = chunk of handshakes):
 //   k_hqc_kg_expand   lane / hs   SE(sk_seed) -> x, y random words; SE(pk_seed) -> h stream
-//   k_hqc_enc_expand  lane / hs   theta = G(m || pk[0:80] || salt); SE(theta) -> r1, r2, e words; SE(pk_seed) -> h
+//   k_hqc_enc_expand  lane / (stream, hs)   theta = G(m || pk[0:80] || salt); SE(theta) -> r1, r2, e words | SE(pk_seed) -> h
 //   k_hqc_dec_expand  lane / hs   SE(sk_seed) -> x, y words (decryption uses y)
 //   k_hqc_kg_mul      WG / hs     s = x + y h; pk = pk_seed || s; sk = sk_seed || sigma || pk
 //   k_hqc_enc_mul     WG / hs     u = r1 + r2 h, v = C.encode(m) + r2 s + e (truncated); ct; K-hash message
@@ -227,20 +227,35 @@ __global__ __launch_bounds__(256) void k_hqc_kg_expand(const uint8_t* __restrict
 }
 
 // row: [r1 RWR][r2 RWR][e RWE][h NHW].  m, pk, salt at arbitrary byte addresses (Encaps:
-// coins / pk; Decaps re-encryption: m' / the pk inside sk / the salt inside ct).
+// coins / pk; Decaps re-encryption: m' / the pk inside sk / the salt inside ct).  Two independent
+// sponges per handshake run on separate lanes (inst = stream * C + hs, C a multiple of 64, so a
+// wave runs one kind): stream 0 theta = G(m || pk[0:80] || salt) then SE(theta) -> r1, r2, e;
+// stream 1 SE(pk_seed) -> h.  Twice the lanes of a lane-per-handshake launch (latency-bound
+// sponges at ~1 wave per SIMD for a 2^16 batch).
 template <int L>
 __global__ __launch_bounds__(256) void k_hqc_enc_expand(const uint8_t* __restrict__ m, size_t m_stride,
                                                         const uint8_t* __restrict__ pk, size_t pk_stride,
                                                         const uint8_t* __restrict__ salt, size_t salt_stride,
-                                                        size_t n, uint64_t* __restrict__ row) {
+                                                        size_t n, size_t C, uint64_t* __restrict__ row) {
   using P = HQ<L>;
   constexpr int KW = P::K / 8, TW = KW + 10 + 2 + 1;  // m || pk[0:80] || salt || (0x03, 0x1F)
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
-  const uint8_t* mp = m + hs * m_stride;
+  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t hs = inst % C;
+  const bool hstream = inst >= C;
+  if (hs >= n || inst >= 2 * C) return;
   const uint8_t* pp = pk + hs * pk_stride;
-  const uint8_t* sp = salt + hs * salt_stride;
   uint64_t* r = row + hs * P::ROWW;
+  KState s;
+  uint64_t sd[5];
+  if (hstream) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) sd[i] = ld64u(pp + 8 * i);
+    seedexp_init(s, sd);
+    squeeze_words(s, r + 2 * P::RWR + P::RWE, P::NHW);
+    return;
+  }
+  const uint8_t* mp = m + hs * m_stride;
+  const uint8_t* sp = salt + hs * salt_stride;
   uint64_t w[TW];
 #pragma unroll
   for (int i = 0; i < KW; ++i) w[i] = ld64u(mp + 8 * i);
@@ -249,17 +264,11 @@ __global__ __launch_bounds__(256) void k_hqc_enc_expand(const uint8_t* __restric
   w[KW + 10] = ld64u(sp);
   w[KW + 11] = ld64u(sp + 8);
   w[KW + 12] = 0x03ull | (0x1Full << 8);
-  KState s;
   shake256_block<TW>(s, w);
-  uint64_t sd[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) sd[i] = kword(s, i);  // theta[0:40]
   seedexp_init(s, sd);
   squeeze_words(s, r, 2 * P::RWR + P::RWE);
-#pragma unroll
-  for (int i = 0; i < 5; ++i) sd[i] = ld64u(pp + 8 * i);
-  seedexp_init(s, sd);
-  squeeze_words(s, r + 2 * P::RWR + P::RWE, P::NHW);
 }
 
 // row: [x words RWW][y words RWW]
@@ -940,8 +949,9 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
                     hipStream_t st) {
   using P = HQ<L>;
   View v = carve<L>(scratch, n);
-  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins,
-             (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, v.row);
+  const size_t C64 = (n + 63) & ~(size_t)63;
+  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, coins,
+             (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, C64, v.row);
   QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, coins,
              pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
              v.msg);
@@ -962,8 +972,9 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
              (size_t)P::MW * 8);
   QRK_LAUNCH("k_hqc_rs", st, k_hqc_rs<L>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n, (const uint8_t*)syms,
              (size_t)P::MW * 8, v.mp);
-  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.mp, (size_t)32,
-             sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row);
+  const size_t C64 = (n + 63) & ~(size_t)63;
+  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, v.mp, (size_t)32,
+             sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, C64, v.row);
   QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row,
              (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
   QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
