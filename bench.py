@@ -376,7 +376,7 @@ def bench_handshake(args, world, rank, local):
     alg = args.alg
     frodo = alg in FP
     hqc = alg in HQ
-    lb = args.log2_batch if args.log2_batch is not None else (14 if frodo else (16 if hqc else 20))
+    lb = args.log2_batch if args.log2_batch is not None else (16 if (frodo or hqc) else 20)
     B = 1 << lb
     drv = HandshakeDriver(alg, symmetric_name=args.symmetric, device=local, chunk=args.chunk)
     e = drv.engine
