@@ -213,10 +213,10 @@ static const AlgInfo* resolve(const char* alg) {
 enum class Op { KEYPAIR, ENCAPS, DECAPS };
 
 // FrodoKEM scratch is 0.14-0.53 MB per handshake, HQC's 9-24 KB: their chunks are capped so
-// scratch stays near QRK_SCRATCH_GIB (32 GiB of the 288 GB HBM by default: a 2^16 FrodoKEM batch in
+// scratch stays near QRK_SCRATCH_GIB (48 GiB of the 288 GB HBM by default: a 2^16 FrodoKEM batch in
 // one chunk, so the lane-per-handshake sponge kernels get a whole wave per SIMD)
 #ifndef QRK_SCRATCH_GIB
-#define QRK_SCRATCH_GIB 32
+#define QRK_SCRATCH_GIB 48
 #endif
 static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
   size_t cap = ctx->chunk;
