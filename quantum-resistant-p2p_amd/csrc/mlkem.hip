@@ -196,7 +196,11 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #ifndef QRK_WPE_FRONT
 #define QRK_WPE_FRONT 1
 #endif
+#ifndef QRK_WPE_XOF
+#define QRK_WPE_XOF 1
+#endif
 #define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
+#define QRK_XOF_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_XOF)))
 #define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
 
 // (a & m) | b as one v_bitop3_b32 (truth table 0xEA): full rate on gfx950, where
@@ -257,7 +261,7 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 // it needs (rewriting identical chunks), so the rare 4th block never idles a
 // whole wave.
 template <int K, bool FIX>
-__global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
+__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
                                              size_t n, size_t C, uint4* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(256) void k_xof(const uint8_t* __restrict__ rho_bas
 // PRF producer: SHAKE256(seed || N) -> 64*eta bytes; inst = N * C + hs.
 // eta = (N < eta1_upto) ? ETA1 : ETA2.
 template <int ETA1, int ETA2>
-__global__ __launch_bounds__(256) void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
+__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
                                              int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
   const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (inst >= (size_t)nprf * C) return;

@@ -36,6 +36,19 @@ def _dptr(t) -> ct.c_void_p:
     return ct.c_void_p(t.data_ptr())
 
 
+def _check_dev(t, width: int, what: str, n: Optional[int] = None):
+    """Device [n, width] uint8 contiguous, like _as_host's check for host arrays: the kernels
+    index rows at the fixed stride `width`, so a wrong shape must fail here, not read past
+    the tensor (the reference raises ValueError on a wrong-length input, oqs.py:341-347)."""
+    if t.dtype != torch.uint8 or t.dim() != 2 or t.shape[1] != width:
+        raise ValueError(f"{what}: expected a [n, {width}] uint8 tensor, got {tuple(t.shape)} {t.dtype}")
+    if n is not None and t.shape[0] != n:
+        raise ValueError(f"{what}: batch size {t.shape[0]} != {n}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    return t
+
+
 def _hptr(a: np.ndarray) -> ct.c_void_p:
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(ct.c_void_p)
@@ -113,7 +126,8 @@ class BatchKEM:
             self._check(LIB.qrk_kem_keypair_batch_host(self._ctx, self._name, n, _hptr(pk), _hptr(sk), _hptr(c)),
                         "keypair")
             return pk, sk
-        n = coins.shape[0] if coins is not None else n
+        if coins is not None:
+            n = _check_dev(coins, self.kp_coins, "keypair coins").shape[0]
         pk, sk = self._empty(n, self.pk_len), self._empty(n, self.sk_len)
         cp = _dptr(coins) if coins is not None else None
         self._check(LIB.qrk_kem_keypair_batch(self._ctx, self._name, n, _dptr(pk), _dptr(sk), cp, self._stream()),
@@ -124,11 +138,13 @@ class BatchKEM:
     def encaps(self, pk, coins=None, return_status: bool = False):
         """Returns (ct, ss) (+ status int32[n]: -1 where pk fails the FIPS 203 7.2 check)."""
         if _is_dev(pk):
-            n = pk.shape[0]
+            n = _check_dev(pk, self.pk_len, "encaps pk").shape[0]
             c, ss = self._empty(n, self.ct_len), self._empty(n, self.ss_len)
             st = torch.empty((n,), dtype=torch.int32, device=pk.device) if return_status else None
             if coins is not None and not _is_dev(coins):
                 coins = torch.from_numpy(_as_host(coins, self.enc_coins)).to(pk.device)
+            if coins is not None:
+                _check_dev(coins, self.enc_coins, "encaps coins", n)
             self._check(LIB.qrk_kem_encaps_batch(self._ctx, self._name, n, _dptr(c), _dptr(ss), _dptr(pk),
                                                  _dptr(coins) if coins is not None else None,
                                                  _dptr(st) if st is not None else None, self._stream()), "encaps")
@@ -149,7 +165,8 @@ class BatchKEM:
         implicit rejection, status 0.  HQC: status -1 where the re-encryption check fails (the
         OQS_ERROR liboqs returns there); ss = K(sigma || ct) is written either way."""
         if _is_dev(sk) and _is_dev(ct_):
-            n = sk.shape[0]
+            n = _check_dev(sk, self.sk_len, "decaps sk").shape[0]
+            _check_dev(ct_, self.ct_len, "decaps ct", n)
             ss = self._empty(n, self.ss_len)
             if return_status:
                 st = torch.empty((n,), dtype=torch.int32, device=sk.device)
@@ -205,6 +222,7 @@ class BatchKEM:
 
     def tamper(self, ct_, seed: int, mode: int) -> None:
         """In-place: mode 0 none, 1 every ciphertext, 2 Bernoulli(1/2) per index."""
+        _check_dev(ct_, self.ct_len, "tamper ct")
         self._check(LIB.qrk_tamper(self._ctx, ct_.shape[0], self.ct_len, seed, mode, _dptr(ct_), self._stream()),
                     "tamper")
 

@@ -51,6 +51,30 @@ def test_bad_arguments_fail_loudly():
     LIB.qrk_ctx_destroy(h)
 
 
+@pytest.mark.parametrize("alg", ["ML-KEM-768", "FrodoKEM-976-SHAKE", "HQC-128"])
+def test_wrong_width_device_tensors_raise(alg):
+    """Device inputs are shape-checked like host ones (a wrong row width would make the
+    kernels read past the tensor): ValueError, as the reference raises on a too-long
+    input (oqs.py:341-347)."""
+    from qrkem.batch import BatchKEM
+    eng = BatchKEM(alg, device=0)
+    d = lambda *s: torch.zeros(s, dtype=torch.uint8, device="cuda")  # noqa: E731
+    with pytest.raises(ValueError):
+        eng.keypair(coins=d(3, eng.kp_coins + 8))
+    pk, sk = eng.keypair(coins=d(3, eng.kp_coins))
+    with pytest.raises(ValueError):
+        eng.encaps(pk[:, 1:].contiguous())
+    with pytest.raises(ValueError):
+        eng.encaps(pk, coins=d(2, eng.enc_coins))
+    c, _ = eng.encaps(pk, coins=d(3, eng.enc_coins))
+    with pytest.raises(ValueError):
+        eng.decaps(sk, c[:2].contiguous())
+    with pytest.raises(ValueError):
+        eng.decaps(sk.view(torch.int8), c)
+    with pytest.raises(ValueError):
+        eng.tamper(d(3, eng.ct_len - 1), seed=1, mode=1)
+
+
 @pytest.mark.parametrize("alg", ["ML-KEM-512", "ML-KEM-1024", "FrodoKEM-976-AES"])
 def test_batch_of_one_matches_single_shot(alg):
     import oracle as orc

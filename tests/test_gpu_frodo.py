@@ -38,7 +38,7 @@ def _host(t):
 
 def _coins(alg, n, seed):
     import oracle as orc
-    kpl, encl = 3 * SEC[alg], SEC[alg]
+    kpl, encl = 2 * SEC[alg] + 16, SEC[alg]  # s || seedSE || z (len_z = 16), mu
     c = orc.bench_coins(n, kpl + encl, seed=seed)
     return np.ascontiguousarray(c[:, :kpl]), np.ascontiguousarray(c[:, kpl:])
 
