@@ -115,3 +115,45 @@ def test_frodo_bench_batch_roundtrip_tamper_and_sample(alg):
     assert np.array_equal(ss3_h, orc.batch_decaps(alg, osk, np.ascontiguousarray(bad_h), 8))
     del pk, sk, ct, ss, ss2, ss3, bad, coins, kc, ec
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("alg", ["HQC-128", "HQC-192", "HQC-256"])
+def test_hqc_bench_batch_roundtrip_tamper_and_sample(alg):
+    """HQC at the bench's 2^16 batch: every ss_enc == ss_dec with status 0, a one-bit tamper
+    on every other ciphertext gives status -1 and a different key on exactly those indices,
+    and a sample of KeyGen / Encaps / tampered Decaps (key and status) is byte-exact vs the
+    C oracle."""
+    import oracle as orc
+    from qrkem.batch import BatchKEM
+    n = 1 << 16
+    eng = BatchKEM(alg, device=0)
+    kpl, encl = eng.kp_coins, eng.enc_coins
+    # bench_coins squeezes one SHAKE256 block (<= 136 B, whole words): one draw per role
+    kc = eng.bench_coins(n, (kpl + 7) // 8 * 8, seed=128)[:, :kpl].contiguous()
+    ec = eng.bench_coins(n, (encl + 7) // 8 * 8, seed=129)[:, :encl].contiguous()
+    coins = None
+    pk, sk = eng.keypair(coins=kc)
+    ct, ss = eng.encaps(pk, coins=ec)
+    ss2, st2 = eng.decaps(sk, ct, return_status=True)
+    bad = ct.clone()
+    eng.tamper(bad, seed=3, mode=2)
+    flip = (bad != ct).any(dim=1)
+    ss3, st3 = eng.decaps(sk, bad, return_status=True)
+    torch.cuda.synchronize()
+    assert bool((ss == ss2).all()) and bool((st2 == 0).all())
+    assert 0.48 < flip.float().mean().item() < 0.52
+    assert bool((ss3[~flip] == ss[~flip]).all()) and bool((st3[~flip] == 0).all())
+    assert not bool((ss3[flip] == ss[flip]).all(dim=1).any())
+    assert bool((st3[flip] == -1).all())
+    idx = np.unique(np.r_[0:4, n // 2 - 2:n // 2 + 2, 0:n:1 << 12, n - 4:n])
+    ti = torch.from_numpy(idx).cuda()
+    pk_h, sk_h, ct_h, ss_h, kc_h, ec_h, bad_h, ss3_h, st3_h = (
+        t.index_select(0, ti).cpu().numpy() for t in (pk, sk, ct, ss, kc, ec, bad, ss3, st3))
+    opk, osk = orc.batch_keypair(alg, np.ascontiguousarray(kc_h), 8)
+    oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h), 8)
+    assert np.array_equal(pk_h, opk) and np.array_equal(sk_h, osk)
+    assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
+    oss3, ost3 = orc.batch_decaps(alg, osk, np.ascontiguousarray(bad_h), 8, with_status=True)
+    assert np.array_equal(ss3_h, oss3) and np.array_equal(st3_h, ost3)
+    del pk, sk, ct, ss, ss2, ss3, bad, coins, kc, ec
+    torch.cuda.empty_cache()
