@@ -185,38 +185,68 @@ def env_int(name, default):
     return int(v) if v not in (None, "") else default
 
 
+def host_cpu() -> dict:
+    """The host cores this job may use and the CPU model (SURVEY.md 8d CPU baseline (ii)).
+    On the GPU box nproc / os.cpu_count() report the whole machine while the job's cgroup
+    quota (cpu.max) allots it a share: the baseline uses every core of that share."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = -(-int(q) // int(period))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cores = min(aff, quota) if quota else aff
+    return {"cores": cores, "model": model, "logical_cpus_on_host": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_quota_cores": quota}
+
+
 def cpu_threads() -> int:
-    n = os.cpu_count() or 1
-    cap = env_int("OMP_NUM_THREADS", 16)
-    return max(1, min(n, cap, 16))
+    return host_cpu()["cores"]
 
 
-def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
-    """Oracle (C restatement, 'port') timed on host cores over a bounded sample (~12 s);
-    also checks the GPU outputs for the sampled indices byte-for-byte.
+def cpu_baseline(alg, mode, kc, pk, sk, ec, ct_in, ss_gpu, B):
+    """Oracle (C restatement, 'port') timed on every host core this job may use, over a bounded
+    sample (~12 s); also checks the GPU outputs for the sampled indices byte-for-byte, KeyGen
+    included (the sample's keys are regenerated on the CPU from the same coins).
     mode "encdec": Encaps(pk, ec) + Decaps; ct_in / ss_gpu = the GPU's ct / ss.
     mode "decaps-tampered": Decaps(sk, ct_in) only; ss_gpu = the GPU's ss."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as orc
-    threads = cpu_threads()
+    cpu = host_cpu()
+    threads = cpu["cores"]
 
     def take(t, n):
         return np.ascontiguousarray(t[:n].cpu().numpy())
 
-    def run(n):
+    def run(n, opk, osk):
         if mode == "encdec":
-            c, s = orc.batch_encaps(alg, take(pk, n), take(ec, n), threads)
-            return c, s, orc.batch_decaps(alg, take(sk, n), c, threads, with_status=True)[0]
-        return None, None, orc.batch_decaps(alg, take(sk, n), take(ct_in, n), threads, with_status=True)[0]
+            c, s = orc.batch_encaps(alg, opk[:n], take(ec, n), threads)
+            return c, s, orc.batch_decaps(alg, osk[:n], c, threads, with_status=True)[0]
+        return None, None, orc.batch_decaps(alg, osk[:n], take(ct_in, n), threads, with_status=True)[0]
 
     cal = min(256 if (alg in FP or alg in HQ) else 1024, B)
+    opk, osk = orc.batch_keypair(alg, take(kc, cal), threads)
     t0 = time.perf_counter()
-    run(cal)
+    run(cal, opk, osk)
     rate = cal / max(time.perf_counter() - t0, 1e-6)
     S = int(min(B, max(cal, (rate * 12.0) // 256 * 256)))
-    sk_s = take(sk, S)
+    # KeyGen of the sample on the CPU (untimed, as on the GPU): the GPU's keys must match
     t0 = time.perf_counter()
-    c, s, s2 = run(S)
+    opk, osk = orc.batch_keypair(alg, take(kc, S), threads)
+    keygen_rate = S / max(time.perf_counter() - t0, 1e-6)
+    keygen_match = bool(np.array_equal(opk, take(pk, S)) and np.array_equal(osk, take(sk, S)))
+    t0 = time.perf_counter()
+    c, s, s2 = run(S, opk, osk)
     dt = time.perf_counter() - t0
     if mode == "encdec":
         match = bool(np.array_equal(c, take(ct_in, S)) and np.array_equal(s, take(ss_gpu, S))
@@ -224,7 +254,7 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
     else:
         match = bool(np.array_equal(s2, take(ss_gpu, S)))
     # the reference call pattern: one handshake per Python call, one core
-    pk_s, ec_s, ct_s = take(pk, S), take(ec, S), take(ct_in, S)
+    pk_s, ec_s, ct_s = opk, take(ec, S), take(ct_in, S)
     t0 = time.perf_counter()
     m = 0
     while time.perf_counter() - t0 < 2.0 and m < S:
@@ -232,7 +262,7 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
             cc, _ = orc.encaps(alg, pk_s[m].tobytes(), ec_s[m].tobytes())
         else:
             cc = ct_s[m].tobytes()
-        orc.decaps_rc(alg, sk_s[m].tobytes(), cc)
+        orc.decaps_rc(alg, osk[m].tobytes(), cc)
         m += 1
     single = m / (time.perf_counter() - t0)
     spec = "FrodoKEM round 3" if alg in FP else ("HQC 2023-04-30" if alg in HQ else "FIPS 203")
@@ -240,9 +270,12 @@ def cpu_baseline(alg, mode, pk, sk, ec, ct_in, ss_gpu, B):
         "value": S / dt, "unit": "encaps+decaps/s" if mode == "encdec" else "decaps/s", "cores": threads,
         "kind": "port",
         "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so, C restatement of "
-                  f"{spec}, -O3 -march=native, {threads} pthreads); liboqs itself is absent "
-                  f"(.MISSING_LARGE_BLOBS:1)",
+                  f"{spec}, -O3 -march=native, {threads} pthreads = every core of this job's host share); "
+                  f"liboqs itself is absent (.MISSING_LARGE_BLOBS:1)",
+        "cpu": cpu,
         "sample_matches_gpu": match,
+        "keygen_sample_matches_gpu": keygen_match,
+        "keygen_per_s": keygen_rate,
         "single_core_python_per_call": single,
     }
 
@@ -445,7 +478,7 @@ def bench_handshake(args, world, rank, local):
         "config": {"workload": f"{alg} batched handshake driver, 2^{lb} exchanges per GPU (SURVEY.md 8f-1)",
                    "alg": alg, "symmetric": args.symmetric, "batch_per_gpu": B, "global_batch": B * world,
                    "mean_info_bytes": info_len, "parallelism": f"index-sharded x{world} (no data-path collective)"},
-        "roofline": roof, "valu_frac_of_peak_step": value * W / VALU_PEAK if W else None, "valu_ops_per_unit": W,
+        "roofline": roof, "valu_frac_of_peak_step": value * W / (VALU_PEAK * world) if W else None, "valu_ops_per_unit": W,
         "kernels_timed_region": kernels, "checks": {"key_disagreements": disagree}, "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -466,7 +499,7 @@ def bench_handshake(args, world, rank, local):
                                                                 (c, out.ciphertext), (key_i, out.key_initiator),
                                                                 (key_r, out.key_responder)))
         result["cpu_baseline"] = {
-            "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port",
+            "value": S / dt, "unit": "handshakes/s", "cores": threads, "kind": "port", "cpu": host_cpu(),
             "sample": f"first {S} handshakes of the same workload (oracle/liboracle.so: "
                       f"{'FrodoKEM round 3' if frodo else ('HQC 2023-04-30' if hqc else 'FIPS 203')} + RFC 5869 C "
                       f"restatement, {threads} pthreads)",
@@ -606,6 +639,9 @@ def main():
     ap.add_argument("--alg", default="ML-KEM-768")
     ap.add_argument("--log2-batch", type=int, default=None, help="default 20 (ML-KEM), 16 (FrodoKEM, HQC)")
     ap.add_argument("--chunk", type=int, default=1 << 20)
+    ap.add_argument("--global-log2-batch", type=int, default=None,
+                    help="BASELINE configs[2]: a fixed global batch of 2^G handshakes split across the ranks "
+                         "(strong scaling, e.g. 24), with per-block digests of every rank's (ct, ss)")
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
@@ -640,19 +676,29 @@ def main():
     if args.mode == "wire":
         return bench_wire(args, world, rank, local)
     from qrkem.batch import BatchKEM
-    from qrkem.shard import reduce_run, weak_shard
+    from qrkem.shard import DIGEST_BLOCK, block_digests, combine_digests, gather_digests, reduce_run, \
+        strong_shard, weak_shard
     alg = args.alg
     frodo = alg in FP
     hqc = alg in HQ
     lb = args.log2_batch if args.log2_batch is not None else (16 if (frodo or hqc) else 20)
     B = 1 << lb
+    strong = args.global_log2_batch is not None
+    if strong:  # configs[2]: 2^G handshakes in total, contiguous index shards
+        if args.mode != "encdec":
+            raise SystemExit("--global-log2-batch: encdec mode only")
+        lb = args.global_log2_batch
+        shard = strong_shard(rank, world, 1 << lb)
+    else:  # weak scaling: 2^lb handshakes per rank, rank r takes [r 2^lb, (r+1) 2^lb)
+        shard = weak_shard(rank, world, B)
+    B = shard.count
     eng = BatchKEM(alg, device=local, chunk=args.chunk)
     if args.streams:
         eng.set_streams(args.streams)
     cap = eng.effective_chunk
     nch = -(-B // cap)
     chunk_eff = min(cap, (-(-B // nch) + 63) // 64 * 64)  # equal chunks, as the library splits them
-    base = weak_shard(rank, world, B).first  # global index range [base, base + B)
+    base = shard.first  # global index range [base, base + B)
 
     kpl, encl = eng.kp_coins, eng.enc_coins
     if kpl + encl <= 136:  # one SHAKE256 block per index
@@ -748,7 +794,7 @@ def main():
         checks["decaps_ms_per_step"] = variants
         checks["tampered_over_valid_time"] = variants["all-tampered"] / variants["all-valid"]
 
-    total = B * world * args.steps
+    total = (1 << lb if strong else B * world) * args.steps
     value = total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     # roofline: kernel durations measured live over the timed region (the schedule as run);
@@ -777,12 +823,13 @@ def main():
 
     W = valu_ops(alg, args.mode)
     headline = alg == "ML-KEM-768" and args.mode == "encdec"
-    cfg_idx = (2 if lb >= 24 else 1) if not frodo and args.mode == "encdec" else (3 if frodo else 4)
+    cfg_idx = (2 if strong else 1) if not frodo and args.mode == "encdec" else (3 if frodo else 4)
     cfg_label = "SURVEY.md 8f-4" if hqc else f"BASELINE.json configs[{cfg_idx}]"
     what = "Encaps+Decaps" if args.mode == "encdec" else "Decaps, 50% tampered (mixed)"
     result = {
-        "metric": METRIC if headline else f"{alg} {'encaps+decaps' if args.mode == 'encdec' else 'decaps'}"
-                                          f"/sec at batch 2^{lb} per GPU",
+        "metric": (f"{alg} encaps+decaps/sec (node) at a fixed global batch of 2^{lb} sharded across the GPUs"
+                   if strong else METRIC if headline else
+                   f"{alg} {'encaps+decaps' if args.mode == 'encdec' else 'decaps'}/sec at batch 2^{lb} per GPU"),
         "value": value,
         "unit": "encaps+decaps/s" if args.mode == "encdec" else "decaps/s",
         "n_gpus": world,
@@ -790,18 +837,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u32 (Keccak, F2[X] words, GF(2^8))" if hqc else "u32" if not frodo else ("u32 (AES T-table) + i8->i32 (MFMA)" if alg.endswith("-AES") else "u32 (Keccak) + i8->i32 (MFMA)"),
         "data": "synthetic: coins = SHAKE256('qrk-bench'||LE64(seed)||LE64(i)) generated on device; "
                 "keys from batched KeyGen on those coins",
-        "config": {"workload": f"{alg} {what} of 2^{lb} device-resident handshakes per GPU "
-                               f"({cfg_label})",
-                   "alg": alg, "batch_per_gpu": B, "global_batch": B * world, "chunk": chunk_eff,
+        "config": {"workload": (f"{alg} {what} of 2^{lb} device-resident handshakes in total, "
+                                f"2^{lb}/{world} per GPU ({cfg_label})" if strong else
+                                f"{alg} {what} of 2^{lb} device-resident handshakes per GPU ({cfg_label})"),
+                   "alg": alg, "batch_per_gpu": B, "global_batch": (1 << lb) if strong else B * world,
+                   "first_index": base, "chunk": chunk_eff,
                    "parallelism": f"index-sharded x{world} (no data-path collective)"},
         "roofline": roof,
         "mfma": mfma,
-        "valu_frac_of_peak_step": value * W / VALU_PEAK,
+        "valu_frac_of_peak_step": value * W / (VALU_PEAK * world),  # per GPU
         "valu_ops_per_unit": W,
         "keygen_per_s": B * world / keygen_s if keygen_s > 0 else None,
         "kernels": kernels,
@@ -809,8 +858,20 @@ def main():
         "checks": checks,
         "cpu_baseline": None,
     }
+    if strong:
+        # per-record SHA3-256(ct_i || ss_i) on the GPU, SHA-256 per block of 2^20 global indices:
+        # the same block digests for every GPU count
+        recs = eng.digest_rows(ct, ss).cpu().numpy()
+        mine = block_digests(recs, base)
+        allb = gather_digests(mine)
+        result["shard_digests"] = {
+            "record": "SHA3-256(ct_i || ss_i)", "block": DIGEST_BLOCK,
+            "block_digest": "SHA-256 over the block's record digests in index order",
+            "blocks": {str(k): v for k, v in sorted(allb.items())},
+            "global": combine_digests(allb), "rank0_blocks": sorted(mine)}
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(alg, args.mode, pk, sk, ec, ct, ss2 if args.mode != "encdec" else ss, B)
+        result["cpu_baseline"] = cpu_baseline(alg, args.mode, kc, pk, sk, ec, ct, ss2 if args.mode != "encdec" else ss,
+                                              B)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -108,6 +108,13 @@ void qrk_ctx_destroy(qrk_ctx *ctx);
 /* Handshakes per internal chunk (scratch = chunk * per-handshake bytes). */
 int qrk_ctx_set_chunk(qrk_ctx *ctx, size_t chunk);
 size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
+/* Zero every buffer of the context that can hold keys or secret intermediates (device
+ * scratch, handshake scratch, device and pinned host staging); synchronous.  Every call
+ * already zeroes the per-handshake key records it leaves in scratch (seeds, m', K', Kbar,
+ * ...) and the staged copies of host secrets; this also clears noise-polynomial
+ * intermediates, which otherwise persist until the next call.  qrk_ctx_destroy does the
+ * same before freeing. */
+int qrk_ctx_cleanse(qrk_ctx *ctx);
 /* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
  * scratch stays near 8 GiB); 0 for an unknown algorithm. */
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
@@ -125,7 +132,9 @@ int qrk_kem_sizes(const char *alg, size_t out[6]);
  * `status` (nullable, device int32[n]) receives -1 for encapsulation keys that
  * fail the FIPS 203 section 7.2 modulus check, else 0.  `stream` is a
  * hipStream_t (NULL = default stream).  Calls are stream-ordered and
- * asynchronous; re-entrant across contexts. */
+ * asynchronous; re-entrant across contexts.  Calls on one context may use
+ * different streams: each call's stream first waits until the previous call on
+ * that context is done with the context's scratch. */
 int qrk_kem_keypair_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *pk, uint8_t *sk,
                           const uint8_t *coins, void *stream);
 int qrk_kem_encaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ct, uint8_t *ss,
@@ -156,6 +165,12 @@ int qrk_bench_coins(qrk_ctx *ctx, size_t n, size_t len, uint64_t seed, uint64_t 
 /* Flip one ciphertext bit per selected index (mode 0 none, 1 all, 2 Bernoulli(1/2)):
  * h_i = SHAKE256("qrk-tamper"||LE64(seed)||LE64(i))[0..8), bit (h_i>>1) mod 8*ctlen. */
 int qrk_tamper(qrk_ctx *ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t *ct, void *stream);
+/* Per-record digests: out_i = SHA3-256(a_i || b_i), 32 bytes, for n records of a_len and
+ * b_len bytes (b may be NULL with b_len = 0).  Device pointers.  The sharded bench hashes
+ * each rank's (ct, ss) records with it and combines them per block of global indices, so
+ * the digests do not depend on the GPU count. */
+int qrk_digest_rows(qrk_ctx *ctx, size_t n, const uint8_t *a, size_t a_len, const uint8_t *b, size_t b_len,
+                    uint8_t *out, void *stream);
 /* HQC fixed-weight supports (the sampling inside KeyGen / Encaps / Decaps, exposed so the
  * duplicate-removal step can be tested on inputs crafted to collide): for each of n vectors,
  * sup[v][i] = i + floor(r[v][i] * (n_HQC - i) / 2^32), then the spec's removal of duplicates.

@@ -136,23 +136,67 @@ struct qrk_ctx {
   size_t hio_bytes = 0;
   hipStream_t io_stream = nullptr;
   int streams = 2;            // 1: serial schedule (kernel timings in isolation), 2: forked
+  hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
+  bool last_valid = false;
   std::mutex mu;
 };
 
-static int ensure_device(int device) {
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count == 0) return fail("no HIP device available (libqrkem has no CPU path)");
-  if (device < 0 || device >= count) return fail("invalid device index");
-  e = hipSetDevice(device);
-  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+// Calls that use a context's scratch are ordered one after another whatever stream each runs
+// on: the new call's stream waits on the event the previous call recorded at its end.  (A
+// device-pointer call on the caller's stream followed by a host-pointer call on the context's
+// own I/O stream would otherwise let the second overwrite scratch the first is still reading.)
+static int ctx_order(qrk_ctx* ctx, hipStream_t st) {
+  if (!ctx->ev_last) {
+    hipError_t e = hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail("hipEventCreate(last use)", e);
+  }
+  if (ctx->last_valid) {
+    hipError_t e = hipStreamWaitEvent(st, ctx->ev_last, 0);
+    if (e != hipSuccess) return hip_fail("hipStreamWaitEvent(last use)", e);
+  }
   return 0;
 }
+// Host-side wait for the previous call's device work (before freeing or refilling buffers it reads).
+static void ctx_quiesce(qrk_ctx* ctx) {
+  if (ctx->last_valid) (void)hipEventSynchronize(ctx->ev_last);
+}
+// Records the end of this call on `st` on every exit path, including early error returns.
+struct LastUse {
+  qrk_ctx* ctx;
+  hipStream_t st;
+  ~LastUse() {
+    if (hipEventRecord(ctx->ev_last, st) == hipSuccess) ctx->last_valid = true;
+  }
+};
 
-static int grow_device(void** p, size_t* have, size_t need, hipStream_t st) {
+// Makes `device` current for the scope of one ABI call and restores the caller's current
+// device on exit, so a call on a context of GPU 3 never leaves the calling thread (and the
+// torch allocations that follow) switched to GPU 3.
+struct DeviceGuard {
+  int prev = -1;
+  int set(int device) {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) return fail("no HIP device available (libqrkem has no CPU path)");
+    if (device < 0 || device >= count) return fail("invalid device index");
+    if (prev < 0 && hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev == device) return 0;
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+    return 0;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+static int grow_device(qrk_ctx* ctx, void** p, size_t* have, size_t need, hipStream_t st) {
   if (*have >= need) return 0;
   if (*p) {
+    ctx_quiesce(ctx);
     (void)hipStreamSynchronize(st);
+    (void)hipMemset(*p, 0, *have);  // the old buffer may hold secret intermediates
     (void)hipFree(*p);
     *p = nullptr;
     *have = 0;
@@ -189,6 +233,14 @@ static size_t scratch_for(const AlgInfo& a, size_t chunk) {
     case Family::MLKEM: return mlkem_scratch_bytes(a, chunk);
     case Family::FRODO: return frodo_scratch_bytes(a, chunk);
     default: return hqc_scratch_bytes(a, chunk);
+  }
+}
+
+static hipError_t cleanse_records(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
+  switch (a.family) {
+    case Family::MLKEM: return mlkem_cleanse(a, n, scratch, st);
+    case Family::FRODO: return frodo_cleanse(a, n, scratch, st);
+    default: return hqc_cleanse(a, n, scratch, st);
   }
 }
 
@@ -238,12 +290,15 @@ struct TimerScope {
 static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
                      const uint8_t* i2, int32_t* status, hipStream_t st) {
   if (n == 0) return 0;
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  if (ctx_order(ctx, st)) return -1;
+  LastUse last_use{ctx, st};
   // equal chunks (multiples of 64) rather than full chunks plus a small tail
   const size_t cap = chunk_for(ctx, a);
   const size_t nchunks = (n + cap - 1) / cap;
   const size_t chunk = std::min(cap, ((n + nchunks - 1) / nchunks + 63) & ~(size_t)63);
-  if (grow_device(&ctx->scratch, &ctx->scratch_bytes, scratch_for(a, chunk), st)) return -1;
+  if (grow_device(ctx, &ctx->scratch, &ctx->scratch_bytes, scratch_for(a, chunk), st)) return -1;
   // coins: NULL -> OS CSPRNG, uploaded to device staging
   const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
   const size_t clen = (op == Op::KEYPAIR) ? a.kp_coins : a.enc_coins;
@@ -251,8 +306,8 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   if (op != Op::DECAPS && coins == nullptr) {
     const size_t bytes = n * clen;
     if (grow_pinned(&ctx->hstage, &ctx->hstage_bytes, bytes)) return -1;
-    if (grow_device((void**)&ctx->dstage, &ctx->dstage_bytes, bytes, st)) return -1;
-    (void)hipStreamSynchronize(st);  // pinned staging may still feed an earlier copy
+    if (grow_device(ctx, (void**)&ctx->dstage, &ctx->dstage_bytes, bytes, st)) return -1;
+    ctx_quiesce(ctx);  // pinned staging may still feed an earlier call's copy
     if (os_random(ctx->hstage, bytes)) return -1;
     hipError_t e = hipMemcpyAsync(ctx->dstage, ctx->hstage, bytes, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync(coins)", e);
@@ -327,6 +382,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
       }
     }
     if (e != hipSuccess) return hip_fail("kernel launch", e);
+    // key material of this chunk (seeds, m', K', Kbar, ...) does not outlive the call
+    e = cleanse_records(a, m, ctx->scratch, st);
+    if (e != hipSuccess) return hip_fail("hipMemsetAsync(cleanse)", e);
   }
   if (synth) {
     hipError_t e = hipStreamSynchronize(st);
@@ -342,7 +400,8 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
 static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2,
                           const uint8_t* i1, const uint8_t* i2, int32_t* status) {
   if (n == 0) return 0;
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   size_t l_o1, l_o2, l_i1, l_i2;
   switch (op) {
     case Op::KEYPAIR: l_o1 = a.pk, l_o2 = a.sk, l_i1 = i1 ? a.kp_coins : 0, l_i2 = 0; break;
@@ -360,7 +419,7 @@ static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
     if (e != hipSuccess) return hip_fail("hipStreamCreate(io)", e);
   }
   hipStream_t st = ctx->io_stream;
-  if (grow_device((void**)&ctx->dio, &ctx->dio_bytes, in_bytes + out_bytes, st)) return -1;
+  if (grow_device(ctx, (void**)&ctx->dio, &ctx->dio_bytes, in_bytes + out_bytes, st)) return -1;
   if (grow_pinned(&ctx->hio, &ctx->hio_bytes, in_bytes + out_bytes)) return -1;
   uint8_t *d_i1 = ctx->dio, *d_i2 = d_i1 + b_i1, *d_o1 = d_i2 + b_i2, *d_o2 = d_o1 + b_o1, *d_st = d_o2 + b_o2;
   uint8_t* h = ctx->hio;
@@ -378,6 +437,22 @@ static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   memcpy(o1, ho, n * l_o1);
   if (l_o2) memcpy(o2, ho + b_o1, n * l_o2);
   if (status) memcpy(status, ho + b_o1 + b_o2, n * l_st);
+  // the staged copies of secret keys, coins and shared secrets do not outlive the call:
+  // KeyGen (coins in, sk out), Encaps (coins in, ss out), Decaps (sk in, ss out)
+  struct Span {
+    size_t off, len;
+  };
+  const Span sec[2] = {op == Op::KEYPAIR   ? Span{0, n * l_i1}
+                       : op == Op::ENCAPS  ? Span{b_i1, n * l_i2}
+                                           : Span{b_i1, n * l_i2},
+                       op == Op::KEYPAIR ? Span{in_bytes + b_o1, n * l_o2}
+                       : op == Op::ENCAPS ? Span{in_bytes + b_o1, n * l_o2}
+                                          : Span{in_bytes, n * l_o1}};
+  for (const Span& z : sec) {
+    if (!z.len) continue;
+    OQS_MEM_cleanse(h + z.off, z.len);
+    (void)hipMemsetAsync(ctx->dio + z.off, 0, z.len, st);
+  }
   return 0;
 }
 
@@ -535,18 +610,42 @@ void OQS_MEM_cleanse(void* ptr, size_t len) {
 int qrk_ctx_create(qrk_ctx** out, int device) {
   if (!out) return fail("null out");
   *out = nullptr;
-  if (ensure_device(device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(device)) return -1;
   qrk_ctx* c = new qrk_ctx();
   c->device = device;
   *out = c;
   return 0;
 }
 
+// Zero every buffer of the context that can hold keys or secret intermediates (device scratch,
+// handshake scratch, device and pinned host staging).  Synchronous.
+static void cleanse_all(qrk_ctx* ctx) {
+  ctx_quiesce(ctx);
+  if (ctx->scratch) (void)hipMemset(ctx->scratch, 0, ctx->scratch_bytes);
+  if (ctx->hs_scratch) (void)hipMemset(ctx->hs_scratch, 0, ctx->hs_scratch_bytes);
+  if (ctx->dio) (void)hipMemset(ctx->dio, 0, ctx->dio_bytes);
+  if (ctx->dstage) (void)hipMemset(ctx->dstage, 0, ctx->dstage_bytes);
+  (void)hipDeviceSynchronize();
+  if (ctx->hio) OQS_MEM_cleanse(ctx->hio, ctx->hio_bytes);
+  if (ctx->hstage) OQS_MEM_cleanse(ctx->hstage, ctx->hstage_bytes);
+}
+
+int qrk_ctx_cleanse(qrk_ctx* ctx) {
+  if (!ctx) return fail("null context");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  cleanse_all(ctx);
+  return 0;
+}
+
 void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->scratch || ctx->dstage || ctx->aux || ctx->dio) {
-    (void)hipSetDevice(ctx->device);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device) == 0) {
     (void)hipDeviceSynchronize();
+    cleanse_all(ctx);
   }
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->hs_scratch) (void)hipFree(ctx->hs_scratch);
@@ -558,6 +657,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
   delete ctx;
 }
 
@@ -676,16 +776,30 @@ int qrk_kem_decaps_batch_status_host(qrk_ctx* ctx, const char* alg, size_t n, ui
 
 int qrk_bench_coins(qrk_ctx* ctx, size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, void* stream) {
   if (!ctx) return fail("null context");
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   hipError_t e = bench_coins(n, len, seed, first, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail("bench_coins", e);
 }
 
 int qrk_tamper(qrk_ctx* ctx, size_t n, size_t ctlen, uint64_t seed, int mode, uint8_t* ct, void* stream) {
   if (!ctx) return fail("null context");
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   hipError_t e = tamper_ciphertexts(n, ctlen, seed, mode, ct, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail("tamper", e);
+}
+
+int qrk_digest_rows(qrk_ctx* ctx, size_t n, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len,
+                    uint8_t* out, void* stream) {
+  if (!ctx) return fail("null context");
+  if (n && (!a || !out || (b_len && !b))) return fail("null buffer");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  hipError_t e = digest_rows(n, a, a_len, b_len ? b : nullptr, b_len, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail("digest_rows", e);
 }
 
 int qrk_hqc_supports(qrk_ctx* ctx, const char* alg, int kind, size_t n, const uint32_t* r, uint32_t* sup,
@@ -694,7 +808,8 @@ int qrk_hqc_supports(qrk_ctx* ctx, const char* alg, int kind, size_t n, const ui
   if (a->family != Family::HQC) return fail(std::string("not an HQC parameter set: ") + alg);
   if (kind != 0 && kind != 1) return fail("kind must be 0 (w) or 1 (w_r = w_e)");
   if (n && (!r || !sup)) return fail("null buffer");
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   hipError_t e = hqc_supports(*a, kind, n, r, sup, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail("hqc_supports", e);
 }
@@ -707,7 +822,8 @@ int qrk_hkdf_sha256_batch(qrk_ctx* ctx, size_t n, const uint8_t* ikm, size_t ikm
   if (salt_len && !salt) return fail("salt_len > 0 with a NULL salt");
   if (n && (!ikm || !okm || (!info && (info_off || info_len)))) return fail("null buffer");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   hipError_t e = hkdf_sha256(n, ikm, ikm_len, ikm_len, salt, salt_len, info, info_off, info_len, okm_len, okm,
                              okm_len, (hipStream_t)stream);
@@ -722,17 +838,28 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
   if (key_len == 0 || key_len > 255 * 32) return fail("key_len must be 1..8160 bytes");
   if (n == 0) return 0;
   if (!pk_i || !pk_r || !ct || !key_i || !key_r) return fail("null output buffer");
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   hipStream_t st = (hipStream_t)stream;
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  if (ctx_order(ctx, st)) return -1;
+  LastUse last_use{ctx, st};
   // Ephemeral secrets of one chunk live in context scratch and are wiped afterwards
   // (the reference keeps them in Python objects: messaging.py:590-600, 809).
   const size_t chunk = chunk_for(ctx, *a);
   const size_t m0 = std::min(chunk, n);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t b_sk = al(m0 * a->sk), b_ss = al(m0 * a->ss);
-  if (grow_device((void**)&ctx->hs_scratch, &ctx->hs_scratch_bytes, 2 * b_sk + 2 * b_ss, st)) return -1;
+  if (grow_device(ctx, (void**)&ctx->hs_scratch, &ctx->hs_scratch_bytes, 2 * b_sk + 2 * b_ss, st)) return -1;
   uint8_t *sk_i = ctx->hs_scratch, *sk_r = sk_i + b_sk, *ss_i = sk_r + b_sk, *ss_r = ss_i + b_ss;
+  // wipes the ephemeral sk / ss on every exit path, error returns included (runs before
+  // last_use records the end of the call)
+  struct Wipe {
+    void* p;
+    size_t bytes;
+    hipStream_t st;
+    ~Wipe() { (void)hipMemsetAsync(p, 0, bytes, st); }
+  } wipe{ctx->hs_scratch, 2 * b_sk + 2 * b_ss, st};
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     auto co = [&](const uint8_t* c, size_t len) { return c ? c + off * len : nullptr; };
@@ -760,15 +887,15 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
       if (e != hipSuccess) return hip_fail("keys_equal", e);
     }
   }
-  hipError_t e = hipMemsetAsync(ctx->hs_scratch, 0, 2 * b_sk + 2 * b_ss, st);
-  return e == hipSuccess ? 0 : hip_fail("hipMemsetAsync(cleanse)", e);
+  return 0;
 }
 
 int qrk_base64_encode_batch(qrk_ctx* ctx, size_t n, const uint8_t* in, size_t in_len, uint8_t* out, void* stream) {
   if (!ctx) return fail("null context");
   if (n && in_len && (!in || !out)) return fail("null buffer");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   hipError_t e = base64_encode(n, in, in_len, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail("base64_encode", e);
@@ -779,7 +906,8 @@ int qrk_base64_decode_batch(qrk_ctx* ctx, size_t n, const uint8_t* in, size_t ou
   if (!ctx) return fail("null context");
   if (n && out_len && (!in || !out)) return fail("null buffer");
   std::lock_guard<std::mutex> lk(ctx->mu);
-  if (ensure_device(ctx->device)) return -1;
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   hipError_t e = hipSuccess;
   if (status && n) e = hipMemsetAsync(status, 0, n * sizeof(int32_t), (hipStream_t)stream);

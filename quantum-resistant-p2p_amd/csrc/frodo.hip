@@ -1085,7 +1085,24 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   return hipGetLastError();
 }
 
+template <int N>
+hipError_t cleanse_t(size_t n, void* scratch, hipStream_t st) {
+  const size_t C = round64(n);
+  const View<N> v = carve<N>(scratch, C);
+  return hipMemsetAsync(v.seeds, 0, (size_t)((uint8_t*)v.aesp - (uint8_t*)v.seeds), st);  // seeds | kk
+}
+
 }  // namespace frodo
+
+hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 640: return frodo::cleanse_t<640>(n, scratch, st);
+    case 976: return frodo::cleanse_t<976>(n, scratch, st);
+    case 1344: return frodo::cleanse_t<1344>(n, scratch, st);
+  }
+  return hipErrorInvalidValue;
+}
 
 size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk) {
   const size_t C = frodo::round64(chunk);

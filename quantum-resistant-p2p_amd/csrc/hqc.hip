@@ -981,7 +981,23 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   return hipGetLastError();
 }
 
+template <int L>
+hipError_t cleanse_t(size_t n, void* scratch, hipStream_t st) {
+  const View v = carve<L>(scratch, n);
+  return hipMemsetAsync(v.msg, 0, (size_t)((uint8_t*)v.st - (uint8_t*)v.msg), st);  // msg | m'
+}
+
 }  // namespace hqc
+
+hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  switch (a.k) {
+    case 128: return hqc::cleanse_t<128>(n, scratch, st);
+    case 192: return hqc::cleanse_t<192>(n, scratch, st);
+    case 256: return hqc::cleanse_t<256>(n, scratch, st);
+  }
+  return hipErrorInvalidValue;
+}
 
 size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk) {
   switch (a.k) {

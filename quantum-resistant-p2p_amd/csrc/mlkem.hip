@@ -1329,6 +1329,13 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
   return mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8;
 }
 
+hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t C = mlkem::round64(n);
+  const mlkem::ScratchView v = mlkem::carve(scratch, a.k, C);
+  return hipMemsetAsync(v.seeds, 0, 16 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar
+}
+
 hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
                          const Streams& st) {
   if (n == 0) return hipSuccess;

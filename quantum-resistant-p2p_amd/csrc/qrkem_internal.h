@@ -51,6 +51,12 @@ struct Scratch {
 size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk);
 size_t frodo_scratch_bytes(const AlgInfo& a, size_t chunk);
 size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
+// Zero the per-handshake key-material records one chunk of n handshakes left in scratch
+// (ML-KEM: seeds, m', K', Kbar; FrodoKEM: seedSE || k || pkh || mu', the hashed key; HQC: the
+// K-hash message m || u || v and m'), stream-ordered: called after every chunk.
+hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
+hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
+hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 
 // Main stream (the caller's) plus an optional side stream and two events used
 // to fork/join independent kernel chains inside one operation.
@@ -90,6 +96,10 @@ hipError_t hqc_supports(const AlgInfo& a, int kind, size_t n, const uint32_t* r,
 
 // SHAKE256("qrk-bench" || LE64(seed) || LE64(first + i), len) for i < n, len <= 136.
 hipError_t bench_coins(size_t n, size_t len, uint64_t seed, uint64_t first, uint8_t* out, hipStream_t st);
+
+// out_i = SHA3-256(a_i || b_i) (32 B per record); b may be NULL with bl = 0.
+hipError_t digest_rows(size_t n, const uint8_t* a, size_t al, const uint8_t* b, size_t bl, uint8_t* out,
+                       hipStream_t st);
 
 // Flip one bit of ct_i for the indices selected by SHAKE256-derived Bernoulli(1/2)
 // (bench config 5).  mode: 0 none, 1 all, 2 mixed.

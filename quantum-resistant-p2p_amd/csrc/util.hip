@@ -68,4 +68,61 @@ hipError_t tamper_ciphertexts(size_t n, size_t ctlen, uint64_t seed, int mode, u
   return hipGetLastError();
 }
 
+// out_i = SHA3-256(a_i || b_i) for n records (a_i = a + i*al, b_i = b + i*bl, bl may be 0):
+// per-record digests of a batch's outputs, from which the sharded bench builds its shard
+// digests (identical whatever the GPU count).  One lane per record;
+// word loads when both lengths are multiples of 8, byte assembly otherwise.
+__device__ __forceinline__ uint64_t rec_word(const uint8_t* a, size_t al, const uint8_t* b, size_t bl, size_t p,
+                                             size_t total, bool words) {
+  if (words && p + 8 <= total) {
+    if (p + 8 <= al) return *(const uint64_t*)(a + p);
+    if (p >= al) return *(const uint64_t*)(b + (p - al));
+  }
+  uint64_t w = 0;
+  for (int j = 0; j < 8; ++j) {
+    const size_t q = p + j;
+    uint64_t v = 0;
+    if (q < al)
+      v = a[q];
+    else if (q < total)
+      v = b[q - al];
+    else if (q == total)
+      v = DS_SHA3;
+    w |= v << (8 * j);
+  }
+  return w;
+}
+
+__global__ __launch_bounds__(256) void k_digest_rows(size_t n, const uint8_t* __restrict__ a, size_t al,
+                                                     const uint8_t* __restrict__ b, size_t bl,
+                                                     uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* ai = a + i * al;
+  const uint8_t* bi = b ? b + i * bl : nullptr;
+  const size_t total = al + bl;
+  const bool words = (al % 8 == 0) && (bl % 8 == 0);
+  const size_t nblk = total / (8 * RW_SHA3_256) + 1;  // the pad always fits in the last block
+  KState s;
+  kzero(s);
+#pragma unroll 1
+  for (size_t blk = 0; blk < nblk; ++blk) {
+#pragma unroll
+    for (int w = 0; w < RW_SHA3_256; ++w) kxor(s, w, rec_word(ai, al, bi, bl, blk * 136 + 8 * w, total, words));
+    if (blk + 1 == nblk) s.a[RW_SHA3_256 - 1].hi ^= 0x80000000u;
+    keccak_f(s);
+  }
+  uint64_t* o = (uint64_t*)(out + i * 32);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) o[w] = kword(s, w);
+}
+
+hipError_t digest_rows(size_t n, const uint8_t* a, size_t al, const uint8_t* b, size_t bl, uint8_t* out,
+                       hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  QRK_LAUNCH("k_digest_rows", st, k_digest_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, a, al, b,
+             bl, out);
+  return hipGetLastError();
+}
+
 }  // namespace qrk

@@ -43,6 +43,7 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_ctx_set_chunk": (ct.c_int, [P, SZ]),
         "qrk_ctx_set_streams": (ct.c_int, [P, ct.c_int]),
         "qrk_ctx_scratch_bytes": (SZ, [P]),
+        "qrk_ctx_cleanse": (ct.c_int, [P]),
         "qrk_ctx_effective_chunk": (SZ, [P, ct.c_char_p]),
         "qrk_kem_sizes": (ct.c_int, [ct.c_char_p, ct.POINTER(SZ)]),
         "qrk_kem_keypair_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P]),
@@ -55,6 +56,7 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_kem_decaps_batch_status_host": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P]),
         "qrk_bench_coins": (ct.c_int, [P, SZ, SZ, ct.c_uint64, ct.c_uint64, P, P]),
         "qrk_tamper": (ct.c_int, [P, SZ, SZ, ct.c_uint64, ct.c_int, P, P]),
+        "qrk_digest_rows": (ct.c_int, [P, SZ, P, SZ, P, SZ, P, P]),
         "qrk_hqc_supports": (ct.c_int, [P, ct.c_char_p, ct.c_int, SZ, P, P, P]),
         "qrk_hkdf_sha256_batch": (ct.c_int, [P, SZ, P, SZ, P, SZ, P, P, SZ, P, SZ, P]),
         "qrk_handshake_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P, P, SZ, SZ, P, P, P, P, P, P, P]),

@@ -220,6 +220,23 @@ class BatchKEM:
                     "bench_coins")
         return out
 
+    def digest_rows(self, a, b=None):
+        """Per-record SHA3-256(a_i || b_i) of device tensors [n, la] / [n, lb] -> [n, 32] uint8
+        (qrk_digest_rows): the records the sharded bench combines into shard digests."""
+        n = a.shape[0]
+        _check_dev(a, a.shape[1], "digest a")
+        if b is not None:
+            _check_dev(b, b.shape[1], "digest b", n)
+        out = self._empty(n, 32)
+        self._check(LIB.qrk_digest_rows(self._ctx, n, _dptr(a), a.shape[1], _dptr(b) if b is not None else None,
+                                        b.shape[1] if b is not None else 0, _dptr(out), self._stream()),
+                    "digest_rows")
+        return out
+
+    def cleanse(self) -> None:
+        """Zero every context buffer that can hold keys or secret intermediates (qrk_ctx_cleanse)."""
+        self._check(LIB.qrk_ctx_cleanse(self._ctx), "cleanse")
+
     def tamper(self, ct_, seed: int, mode: int) -> None:
         """In-place: mode 0 none, 1 every ciphertext, 2 Bernoulli(1/2) per index."""
         _check_dev(ct_, self.ct_len, "tamper ct")

@@ -78,7 +78,13 @@ def kem_sizes(alg_name: str) -> dict:
     return dict(zip(keys, (int(v) for v in out)))
 
 
-_LEVEL = {"512": 1, "768": 3, "1024": 5, "640": 1, "976": 3, "1344": 5}
+class _KemPrefix(ct.Structure):
+    """Leading fields of the C ``OQS_KEM`` struct (include/qrkem.h), the prefix the reference's
+    wrapper reads from the handle (oqs.py:241-253, 273-280)."""
+    _fields_ = [("method_name", ct.c_char_p), ("alg_version", ct.c_char_p),
+                ("claimed_nist_level", ct.c_ubyte), ("ind_cca", ct.c_ubyte),
+                ("length_public_key", ct.c_size_t), ("length_secret_key", ct.c_size_t),
+                ("length_ciphertext", ct.c_size_t), ("length_shared_secret", ct.c_size_t)]
 
 
 def _fixed(data: Union[bytes, bytearray, memoryview], size: int) -> ct.Array:
@@ -98,15 +104,19 @@ class KeyEncapsulation:
         self._kem = LIB.OQS_KEM_new(alg_name.encode())
         if not self._kem:
             raise RuntimeError(f"OQS_KEM_new({alg_name}) failed: {last_error()}")
+        # every attribute comes from the handle's struct, as oqs.py:273-280 reads it
+        k = ct.cast(self._kem, ct.POINTER(_KemPrefix)).contents
         sz = kem_sizes(alg_name)
-        self.method_name = alg_name.encode()
-        self.alg_version = b"qrkem-gfx950"
-        self.claimed_nist_level = _LEVEL.get(alg_name.split("-")[2 if alg_name.startswith("ML-") else 1], 0)
-        self.ind_cca = 1
-        self.length_public_key = sz["length_public_key"]
-        self.length_secret_key = sz["length_secret_key"]
-        self.length_ciphertext = sz["length_ciphertext"]
-        self.length_shared_secret = sz["length_shared_secret"]
+        self._kp_coins = sz["length_keypair_coins"]
+        self._enc_coins = sz["length_encaps_coins"]
+        self.method_name = k.method_name
+        self.alg_version = k.alg_version
+        self.claimed_nist_level = int(k.claimed_nist_level)
+        self.ind_cca = int(k.ind_cca)
+        self.length_public_key = int(k.length_public_key)
+        self.length_secret_key = int(k.length_secret_key)
+        self.length_ciphertext = int(k.length_ciphertext)
+        self.length_shared_secret = int(k.length_shared_secret)
         self.details = {
             "name": alg_name,
             "version": self.alg_version.decode(),
@@ -134,12 +144,21 @@ class KeyEncapsulation:
         return bytes(pk)
 
     def generate_keypair_derand(self, coins: bytes) -> bytes:
-        """Deterministic KeyGen from explicit coins (d||z for ML-KEM)."""
+        """Deterministic KeyGen from explicit coins (d||z for ML-KEM, s||seedSE||z for FrodoKEM)."""
+        coins = self._coins(coins, self._kp_coins, "keypair")
         pk = ct.create_string_buffer(self.length_public_key)
         self.secret_key = ct.create_string_buffer(self.length_secret_key)
         if LIB.OQS_KEM_keypair_derand(self._kem, pk, self.secret_key, bytes(coins)) != OQS_SUCCESS:
             raise RuntimeError("Can not generate keypair")
         return bytes(pk)
+
+    @staticmethod
+    def _coins(coins, want: int, what: str) -> bytes:
+        # the library reads exactly `want` bytes: a shorter buffer would be read past its end
+        c = bytes(coins)
+        if len(c) != want:
+            raise ValueError(f"{what} coins must be {want} bytes, got {len(c)}")
+        return c
 
     def export_secret_key(self) -> bytes:
         return bytes(self.secret_key)
@@ -153,6 +172,7 @@ class KeyEncapsulation:
         return bytes(c), bytes(ss)
 
     def encap_secret_derand(self, public_key: bytes, coins: bytes) -> tuple[bytes, bytes]:
+        coins = self._coins(coins, self._enc_coins, "encaps")
         pk = _fixed(public_key, self.length_public_key)
         c = ct.create_string_buffer(self.length_ciphertext)
         ss = ct.create_string_buffer(self.length_shared_secret)

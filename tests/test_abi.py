@@ -125,3 +125,35 @@ def test_encap_secret_length_semantics():
     k = oqs.KeyEncapsulation("ML-KEM-512")
     with pytest.raises(ValueError):
         k.encap_secret(bytes(801))
+
+
+LEVELS = {"ML-KEM-512": 1, "ML-KEM-768": 3, "ML-KEM-1024": 5, "FrodoKEM-640-AES": 1, "FrodoKEM-640-SHAKE": 1,
+          "FrodoKEM-976-AES": 3, "FrodoKEM-976-SHAKE": 3, "FrodoKEM-1344-AES": 5, "FrodoKEM-1344-SHAKE": 5,
+          "HQC-128": 1, "HQC-192": 3, "HQC-256": 5}
+
+
+@pytest.mark.parametrize("alg", sorted(LEVELS))
+def test_details_claimed_level_from_struct(alg):
+    """details / attributes come from the OQS_KEM struct, as oqs.py:273-280 reads them (HQC's
+    '128' is a security-bit count, not a level: the struct says 1/3/5)."""
+    from qrkem import oqs
+    k = oqs.KeyEncapsulation(alg)
+    assert k.claimed_nist_level == LEVELS[alg] and k.details["claimed_nist_level"] == LEVELS[alg]
+    assert k.method_name.decode() == alg and k.details["name"] == alg
+    s = oqs.kem_sizes(alg)
+    assert (k.length_public_key, k.length_secret_key, k.length_ciphertext, k.length_shared_secret) == (
+        s["length_public_key"], s["length_secret_key"], s["length_ciphertext"], s["length_shared_secret"])
+    k.free()
+
+
+@pytest.mark.parametrize("alg", ["ML-KEM-768", "FrodoKEM-976-SHAKE", "HQC-128"])
+def test_derand_coins_length_checked(alg):
+    """The library reads exactly the coin length: a wrong-length seed raises instead of being
+    read past its end."""
+    from qrkem import oqs
+    k = oqs.KeyEncapsulation(alg)
+    s = oqs.kem_sizes(alg)
+    with pytest.raises(ValueError, match="keypair coins"):
+        k.generate_keypair_derand(bytes(s["length_keypair_coins"] - 1))
+    with pytest.raises(ValueError, match="encaps coins"):
+        k.encap_secret_derand(bytes(s["length_public_key"]), bytes(s["length_encaps_coins"] + 1))

@@ -78,12 +78,14 @@ def test_full_batch_tampered_decaps_1024():
 FRODO_SEC = {"640": 16, "976": 24, "1344": 32}
 
 
-@pytest.mark.parametrize("alg", ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-640-AES",
-                                 "FrodoKEM-976-AES"])
+@pytest.mark.parametrize("alg", ["FrodoKEM-640-SHAKE", "FrodoKEM-976-SHAKE", "FrodoKEM-1344-SHAKE",
+                                 "FrodoKEM-640-AES", "FrodoKEM-976-AES", "FrodoKEM-1344-AES"])
 def test_frodo_bench_batch_roundtrip_tamper_and_sample(alg):
     """configs[3] at the bench's FrodoKEM batch (2^16 in one chunk): every ss_enc == ss_dec,
     a one-bit tamper on every other ciphertext always rejects, and a sample of KeyGen /
-    Encaps / tampered Decaps is byte-exact vs the C oracle."""
+    Encaps / tampered Decaps is byte-exact vs the C oracle.  The sample holds every
+    1024-th index, both sides of the 2^15 midpoint and the tail (the indices a round-1
+    scratch run flagged, DESIGN.md section 8: a harness coin-width error, not a kernel one)."""
     import oracle as orc
     from qrkem.batch import BatchKEM
     n = 1 << 16
@@ -104,15 +106,17 @@ def test_frodo_bench_batch_roundtrip_tamper_and_sample(alg):
     assert 0.48 < flip.float().mean().item() < 0.52
     assert bool((ss3[~flip] == ss[~flip]).all())
     assert not bool((ss3[flip] == ss[flip]).all(dim=1).any())
-    idx = np.unique(np.r_[0:4, n // 2 - 2:n // 2 + 2, 0:n:1 << 13, n - 4:n])
+    idx = np.unique(np.r_[0:4, n // 2 - 2:n // 2 + 2, 0:n:1 << 10, 1023:n:1 << 10, n - 4:n])
     ti = torch.from_numpy(idx).cuda()
     pk_h, sk_h, ct_h, ss_h, kc_h, ec_h, bad_h, ss3_h = (
         t.index_select(0, ti).cpu().numpy() for t in (pk, sk, ct, ss, kc, ec, bad, ss3))
-    opk, osk = orc.batch_keypair(alg, np.ascontiguousarray(kc_h), 8)
-    oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h), 8)
-    assert np.array_equal(pk_h, opk) and np.array_equal(sk_h, osk)
+    opk, osk = orc.batch_keypair(alg, np.ascontiguousarray(kc_h), 16)
+    bad_pk = idx[(pk_h != opk).any(axis=1)]
+    bad_sk = idx[(sk_h != osk).any(axis=1)]
+    assert bad_pk.size == 0 and bad_sk.size == 0, (bad_pk[:8], bad_sk[:8])
+    oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h), 16)
     assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
-    assert np.array_equal(ss3_h, orc.batch_decaps(alg, osk, np.ascontiguousarray(bad_h), 8))
+    assert np.array_equal(ss3_h, orc.batch_decaps(alg, osk, np.ascontiguousarray(bad_h), 16))
     del pk, sk, ct, ss, ss2, ss3, bad, coins, kc, ec
     torch.cuda.empty_cache()
 
