@@ -321,6 +321,25 @@ def pmc_issued(alg, mode, chunk, kernel):
     return None, None
 
 
+def pmc_mfma(alg, mode, chunk, kernel):
+    """Counter-derived MFMA utilisation of `kernel` from the committed rocprofv3 MFMA pass of the
+    same configuration (profiles/mfma_util.json, written by tools/mfma_summary.py), or None."""
+    idx = ROOT / "profiles" / "mfma_util.json"
+    if not idx.exists():
+        return None
+    e = json.loads(idx.read_text()).get(f"{alg}|{mode}|{chunk}")
+    if not e:
+        return None
+    for k, v in e["kernels"].items():
+        if k == kernel or k.startswith(kernel + "<"):
+            return {"mfma_util": v.get("mfma_util"), "mfma_i8_instrs_per_launch": v.get("mfma_i8_instrs_per_dispatch"),
+                    "int8_ops_per_launch": v.get("int8_ops_per_dispatch"), "achieved_Tops": v.get("achieved_Tops"),
+                    "frac": v.get("frac_of_int8_peak"), "source": e["source"],
+                    "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 1024 SIMDs); "
+                                  "int8 ops = SQ_INSTS_VALU_MFMA_MOPS_I8 x 512 over the traced kernel time"}
+    return None
+
+
 def kernel_report(alg, mode, prof, B):
     """Per-kernel algorithmic rate: ops per handshake x B / total kernel time in `prof`
     (HIP-event durations).  Returns (kernels, roofline-of-dominant, mfma-object-or-None)."""
@@ -802,6 +821,8 @@ def main():
     _, roof, mfma = kernel_report(alg, args.mode, prof_live, B * args.steps)
     kernels, roof_iso, _ = kernel_report(alg, args.mode, prof, B)
     if roof is not None:
+        if mfma is not None:
+            mfma["counters"] = pmc_mfma(alg, args.mode, chunk_eff, mfma["kernel"].split()[0])
         tb, src = pmc_traffic(alg, args.mode, chunk_eff, roof["kernel"])
         roof["traffic"] = tb
         roof["traffic_unit"] = "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"

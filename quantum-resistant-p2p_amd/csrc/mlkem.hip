@@ -156,10 +156,20 @@ __device__ __forceinline__ size_t tidx(size_t inst, int w, int W) {
 
 // 16-lane group synchronisation: a group never spans two waves, so ordering
 // LDS traffic inside the wave is enough.
+#ifndef QRK_GSYNC_FENCE
+#define QRK_GSYNC_FENCE 1
+#endif
 __device__ __forceinline__ void gsync() {
+#if QRK_GSYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#else
+  // The LDS unit performs one wave's DS instructions in issue order, so a lane's read
+  // issued after another lane's write of the same wave observes it without waiting for
+  // the write to complete; the wave barrier keeps the compiler from reordering them.
+  __builtin_amdgcn_wave_barrier();
+#endif
 }
 
 // 8 consecutive 12-bit fields of the little-endian 96-bit string w0|w1|w2
@@ -200,6 +210,14 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #define QRK_WPE_XOF 1
 #endif
 #define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
+// QRK_XOF_CMP 0 (sign-mask acceptance, three full-rate ops per candidate) measured no faster
+// than v_cmp + v_cndmask in k_xof (profiles/r2/ab_xof_signmask_rejected.jsonl)
+#ifndef QRK_XOF_CMP
+#define QRK_XOF_CMP 1
+#endif
+#ifndef QRK_ENC_PREFETCH
+#define QRK_ENC_PREFETCH 1
+#endif
 #define QRK_XOF_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_XOF)))
 #define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
 
@@ -214,6 +232,14 @@ __device__ __forceinline__ uint32_t and_or3(uint32_t a, uint32_t m, uint32_t b) 
 __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
   uint32_t r;
   asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
+  return r;
+}
+
+// x < 0 ? -1 : 0 as one v_ashrrev_i32 (inline asm, so the compiler keeps the mask arithmetic
+// instead of turning it back into v_cmp + v_cndmask)
+__device__ __forceinline__ int sign_mask(int x) {
+  int r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
   return r;
 }
 
@@ -241,7 +267,14 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       *(uint32_t*)(ring_all + and_or3(pos, 0xF00u, rb)) = (uint32_t)c[e];
+#if QRK_XOF_CMP
       pos += c[e] < Q ? 256 : 0;
+#else
+      // accept iff c < q: the sign of c - q, as an all-ones / zero mask, selects the 256-B
+      // ring step -- three full-rate ops in place of v_cmp + v_cndmask, whose VCC round trip
+      // issues at a fraction of the VALU rate (profiles/r1/valu_peak_r1b.json)
+      pos += sign_mask(c[e] - Q) & 256;
+#endif
     }
     cnt = pos >> 8;
     const int ch = before >> 3;
@@ -1107,23 +1140,34 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
     }
   }
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
-  // Row i+1's matrix entries and the next CBD words are loaded one row ahead.
+  // QRK_ENC_PREFETCH: row i+1's matrix entries and the next CBD words are loaded one row
+  // ahead (latency hidden inside the wave); 0: each entry is loaded as the basemul needs it
+  // (fewer live registers, latency hidden by more resident waves).
+#if QRK_ENC_PREFETCH
   PK8 an[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)j * C + hs, L);
+#endif
   CbdRaw er = cbd_load<P<K>::ETA2>(prf, (size_t)K * C + hs, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
+#if QRK_ENC_PREFETCH
 #pragma unroll
     for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
+#else
+#pragma unroll
+    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(i * K + j) * C + hs, L), yb[j]);
+#endif
     const CbdRaw ecur = er;
+#if QRK_ENC_PREFETCH
     if (i + 1 < K) {
 #pragma unroll
       for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hs, L);
     }
+#endif
     er = cbd_load<P<K>::ETA2>(prf, (size_t)(K + i + 1) * C + hs, L);  // e1_{i+1}, or e2 after the last row
     PF16 uf;
 #pragma unroll
