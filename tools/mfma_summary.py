@@ -2,8 +2,10 @@
 """Summarise a tools/pmc_mfma.sh pass: per kernel, int8 MFMA instructions, MFMA MOPs
 (SQ_INSTS_VALU_MFMA_MOPS_I8 counts 512 int8 ops each, the unit of rocprofiler-sdk's derived
 MFMA FLOP counters), MFMA-pipe busy cycles and the derived utilisation
-MFMA_UTIL = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMD count) (rocprofiler-sdk
-counter_defs.yaml).  Kernel durations come from a --kernel-trace summary of the same
+MFMA_UTIL = SQ_VALU_MFMA_BUSY_CYCLES / (max-over-XCDs GRBM_GUI_ACTIVE x SIMD count)
+(rocprofiler-sdk counter_defs.yaml: reduce(GRBM_GUI_ACTIVE, max)).  The CSV value of
+GRBM_GUI_ACTIVE is the sum over the 8 XCD instances, so it is divided by 8 here (the
+per-XCD value then matches the traced kernel time at ~2.3 GHz).  Kernel durations come from a --kernel-trace summary of the same
 configuration (tools/prof_summary.py output) to turn MOPs into an achieved int8 op rate.
 
 usage: tools/mfma_summary.py <gpurun_out/mfma_tag> <trace summary json> <out.json> <alg|mode|chunk>
@@ -17,6 +19,7 @@ from collections import defaultdict
 from pathlib import Path
 
 SIMDS = 256 * 4
+XCDS = 8
 MFMA_I8_PEAK = 5.0e15
 
 
@@ -43,9 +46,12 @@ def main():
              "mfma_busy_cycles_per_dispatch": avg.get("SQ_VALU_MFMA_BUSY_CYCLES"),
              "gui_active_cycles_per_dispatch": avg.get("GRBM_GUI_ACTIVE"),
              "valu_instrs_per_dispatch": avg.get("SQ_INSTS_VALU")}
-        if e["mfma_busy_cycles_per_dispatch"] and e["gui_active_cycles_per_dispatch"]:
-            e["mfma_util"] = e["mfma_busy_cycles_per_dispatch"] / (e["gui_active_cycles_per_dispatch"] * SIMDS)
         t = tr.get(k, {}).get("avg_ms")
+        if e["mfma_busy_cycles_per_dispatch"] and e["gui_active_cycles_per_dispatch"]:
+            e["mfma_util"] = e["mfma_busy_cycles_per_dispatch"] / (e["gui_active_cycles_per_dispatch"] / XCDS * SIMDS)
+        t = tr.get(k, {}).get("avg_ms")
+        if t and e["gui_active_cycles_per_dispatch"]:
+            e["clock_GHz_from_gui_active"] = e["gui_active_cycles_per_dispatch"] / XCDS / (t * 1e-3) / 1e9
         if t and e["mfma_mops_i8_per_dispatch"]:
             ops = e["mfma_mops_i8_per_dispatch"] * 512
             e["avg_ms"] = t
