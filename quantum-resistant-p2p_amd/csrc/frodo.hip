@@ -35,6 +35,13 @@ namespace frodo {
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int NBAR = 8;
+// KeyGen B = AS + E for FrodoKEM-SHAKE: 1 = fused Gen(A) + i8 MFMA (k_fr_kg_mm), 0 = VALU rows
+#ifndef QRK_FR_KG_MM
+#define QRK_FR_KG_MM 1
+#endif
+#ifndef QRK_KG_ACC_VALU
+#define QRK_KG_ACC_VALU 0
+#endif
 constexpr int ST_PITCH = 72;  // LDS pitch (u16) of one column of a 64-row A block: 144 B -> conflict-free 16-B reads
 
 template <int N_>
@@ -100,7 +107,7 @@ template <int N>
 size_t scratch_bytes_t(size_t C) {
   using P = FP<N>;
   const size_t W = (size_t)(P::SE_WORDS > P::KG_WORDS ? P::SE_WORDS : P::KG_WORDS);
-  return al256(C * W * 8) + al256(C * 8 * P::NP) + al256(C * 8 * N * 2) + al256(C * 64 * 2) +
+  return al256(C * W * 8) + al256(C * 8 * P::NP + 256) + al256(C * 8 * N * 2) + al256(C * 64 * 2) +
          al256(C * P::NWV * 8 * N * 2) + al256(C * 128) + al256(C * 32) + al256(C * aes::prep_words<N>() * 4);
 }
 
@@ -113,7 +120,7 @@ View<N> carve(void* base, size_t C) {
   v.raw = (uint64_t*)p;
   p += al256(C * W * 8);
   v.sp8 = (int8_t*)p;
-  p += al256(C * 8 * P::NP);
+  p += al256(C * 8 * P::NP + 256);  // + slack: k_fr_kg_mm reads up to 128 B past a row
   v.ep16 = (int16_t*)p;
   p += al256(C * 8 * N * 2);
   v.epp16 = (int16_t*)p;
@@ -882,6 +889,118 @@ __global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ 
                  __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
 }
 
+// KeyGen B = A S + E (mod 2^16), Gen(A) fused with the product on i8 MFMA (SHAKE128 A).
+// One wave owns 64 consecutive rows of one handshake (lane = row r squeezes row r of A).
+// Each SHAKE128 block's 84 columns go to LDS row-major, one byte per (row, column) and limb
+// (balanced limbs: lo = a & 0xFF, hi = ((a + 128) >> 8) & 0xFF, a == 256 hi + lo mod 2^16),
+// and are contracted over the columns:
+//   D(16x16) = X(16 rows x 64 cols) . Y(64 cols x 16),  X[r][c] = limb(A[r][c]),
+//   Y[c][k] = S[c][k] (k < 8 used; S^T rows from sp8),
+// four 16-row tiles x two 64-column halves (the second half holds columns 64..83, the rest of
+// the stage is zero) x two limbs = 16 MFMAs per block, i32 accumulation over all N columns
+// (|acc| <= N * 128 * 12 < 2^31).  Lane l supplies the same K slice 16 (l >> 4) .. +15 of X
+// and Y, so the hardware's order inside a fragment does not matter.  B = lo + 256 hi + E.
+// LDS row pitch (bytes): 25 dwords (odd, so the 64 lanes' dword writes hit distinct banks),
+// holding the block's 84 columns and 16 zero columns; the second K half's slices past column
+// 96 are zero registers, not LDS
+constexpr int KG_RP = 100;
+template <int N>
+__global__ __launch_bounds__(64) void k_fr_kg_mm(const uint8_t* __restrict__ pk, size_t n,
+                                                 const int8_t* __restrict__ sp8, const int16_t* __restrict__ e16,
+                                                 uint16_t* __restrict__ bmat) {
+  using P = FP<N>;
+  __shared__ __attribute__((aligned(16))) uint8_t st[2][64 * KG_RP];
+  const size_t hs = blockIdx.x / P::NWV;
+  const int wv = (int)(blockIdx.x % P::NWV);
+  if (hs >= n) return;
+  const int lane = threadIdx.x;
+  const int r = wv * 64 + lane;
+  const int kq = lane & 15, ks = 16 * (lane >> 4);
+  // zero the stage once: columns 84..99 of every row stay zero
+  for (int i = lane; i < 2 * 64 * KG_RP / 4; i += 64) ((uint32_t*)st)[i] = 0u;
+  const uint8_t* sa = pk + hs * P::PK;
+  uint64_t in[3];
+  {
+    const uint64_t s0 = ((const uint64_t*)sa)[0], s1 = ((const uint64_t*)sa)[1];
+    in[0] = (uint64_t)(r & 0xFFFF) | (s0 << 16);
+    in[1] = (s0 >> 48) | (s1 << 16);
+    in[2] = s1 >> 48;
+  }
+  KState s;
+  kzero(s);
+  absorb_short<21, 3>(s, in, 18);
+  const int8_t* sk = sp8 + (hs * NBAR + (kq & 7)) * P::NP;  // S^T row kq (k < 8)
+  v4i acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = (v4i){0, 0, 0, 0};
+  uint32_t* row_lo = (uint32_t*)(st[0] + lane * KG_RP);
+  uint32_t* row_hi = (uint32_t*)(st[1] + lane * KG_RP);
+#pragma unroll 1
+  for (int b = 0; b < P::A_BLOCKS; ++b) {
+    if (b) keccak_f(s);
+    const int c0 = 84 * b;
+    const int nc = (N - c0) < 84 ? (N - c0) : 84;  // a multiple of 4 for every parameter set
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int w = 0; w < 21; ++w) {
+      // values 4w .. 4w+3 of this row: lo limbs -> one dword, hi limbs -> one dword
+      const uint32_t lo = s.a[w].lo, hi = s.a[w].hi;
+      const uint32_t lo80 = add80(lo), hi80 = add80(hi);
+      const bool ok = 4 * w < nc && r < N;  // columns past the row's end and rows past N: zero
+      row_lo[w] = ok ? __builtin_amdgcn_perm(hi, lo, 0x06040200u) : 0u;
+      row_hi[w] = ok ? __builtin_amdgcn_perm(hi80, lo80, 0x07050301u) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // Y: S^T row (kq & 7) at this lane's 16 columns of each K half, loaded without conditions
+    // (columns past N read zero padding, the next row or the scratch slack after sp8 -- all
+    // paired with zero X; lanes kq >= 8 feed output columns that are discarded)
+    const v4i y0 = *(const v4i*)(sk + c0 + ks), y1 = *(const v4i*)(sk + c0 + 64 + ks);
+    // X slices reaching past column 99 of the stage (64 + ks >= 96) read the zero columns
+    // 84..99 instead (a slice that crossed the pitch would read the next row)
+    const int xo1 = (64 + ks + 16 <= KG_RP) ? 64 + ks : 84;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int off = (16 * t + kq) * KG_RP + (h ? xo1 : ks);
+        v4i xl, xh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          xl[q] = *(const int*)(st[0] + off + 4 * q);
+          xh[q] = *(const int*)(st[1] + off + 4 * q);
+        }
+#if QRK_KG_ACC_VALU
+        const v4i zr = {0, 0, 0, 0};
+        acc[t][0] += __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, h ? y1 : y0, zr, 0, 0, 0);
+        acc[t][1] += __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, h ? y1 : y0, zr, 0, 0, 0);
+#else
+        acc[t][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, h ? y1 : y0, acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, h ? y1 : y0, acc[t][1], 0, 0, 0);
+#endif
+      }
+    }
+  }
+  // D[m][n]: m = row 16 t + 4 (lane >> 4) + g, n = k = lane & 15
+  if (kq < NBAR) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int rr = wv * 64 + 16 * t + 4 * (lane >> 4) + g;
+        if (rr < N) {
+          const size_t o = ((size_t)hs * N + rr) * NBAR + kq;
+          const uint32_t v = (uint32_t)acc[t][0][g] + ((uint32_t)acc[t][1][g] << 8) + (uint32_t)(int)e16[o];
+          bmat[o] = (uint16_t)(v & P::QMASK);
+        }
+      }
+    }
+  }
+}
+
 // Workgroup size of the AES KeyGen rows kernel: all rows of a handshake in as few
 // workgroups as possible (at most 1024 threads), whole waves.
 template <int N>
@@ -1070,12 +1189,16 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
   uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
-  QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
+  if (AES || !QRK_FR_KG_MM)
+    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
   if constexpr (AES) {
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
                (size_t)P::PK, n, v.aesp);
     QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())), dim3(kg_threads<N>()),
                0, st, v.aesp, n, spair, v.ep16, v.part);
+  } else if (QRK_FR_KG_MM) {
+    QRK_LAUNCH("k_fr_kg_mm", st, k_fr_kg_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, pk, n, v.sp8, v.ep16,
+               v.part);
   } else {
     QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
                spair, v.ep16, v.part);
