@@ -664,7 +664,8 @@ def main():
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
-    ap.add_argument("--streams", type=int, default=0, help="1: serial kernel schedule, 2: forked (default)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="library schedule: 0 auto (serial at full chunks), 1 serial, 2 forked")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -712,8 +713,7 @@ def main():
         shard = weak_shard(rank, world, B)
     B = shard.count
     eng = BatchKEM(alg, device=local, chunk=args.chunk)
-    if args.streams:
-        eng.set_streams(args.streams)
+    eng.set_streams(args.streams)
     cap = eng.effective_chunk
     nch = -(-B // cap)
     chunk_eff = min(cap, (-(-B // nch) + 63) // 64 * 64)  # equal chunks, as the library splits them
@@ -788,7 +788,7 @@ def main():
         torch.cuda.synchronize()
         prof = dict(eng.profile_read().items())
         eng.profile(False)
-        eng.set_streams(args.streams or 2)
+        eng.set_streams(args.streams)
 
     ct, ss, ss2 = out
     if args.mode == "encdec":

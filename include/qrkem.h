@@ -118,9 +118,10 @@ int qrk_ctx_cleanse(qrk_ctx *ctx);
 /* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
  * scratch stays near 8 GiB); 0 for an unknown algorithm. */
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
-/* 2 (default): independent kernel chains of one operation run forked on a
- * side stream and join the caller's stream; 1: everything on the caller's
- * stream (kernel timings in isolation). */
+/* 0 (default, auto): independent kernel chains of one operation run forked on
+ * a side stream and join the caller's stream when a chunk is below 65536
+ * handshakes (latency), serially above (throughput); 2: always forked; 1:
+ * always serial (kernel timings in isolation). */
 int qrk_ctx_set_streams(qrk_ctx *ctx, int streams);
 
 /* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */

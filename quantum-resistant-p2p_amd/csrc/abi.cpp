@@ -135,7 +135,7 @@ struct qrk_ctx {
   uint8_t* hio = nullptr;         // ... and their pinned host mirror
   size_t hio_bytes = 0;
   hipStream_t io_stream = nullptr;
-  int streams = 2;            // 1: serial schedule (kernel timings in isolation), 2: forked
+  int streams = 0;            // 0: auto (forked below QRK_FORK_MAX per chunk), 1: serial, 2: forked
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
   bool last_valid = false;
   std::mutex mu;
@@ -217,6 +217,10 @@ static int grow_pinned(uint8_t** p, size_t* have, size_t need) {
   *have = need;
   return 0;
 }
+
+#ifndef QRK_FORK_MAX
+#define QRK_FORK_MAX 65536
+#endif
 
 static int os_random(uint8_t* out, size_t n) {
   while (n) {
@@ -323,7 +327,11 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   Streams S;
   S.main = st;
   // (the fork also shortens single-shot latency: the SampleNTT chain runs beside front + PRF)
-  S.aux = ctx->streams > 1 ? ctx->aux : nullptr;
+  // The fork overlaps the SampleNTT chain with the front/PRF chain: it shortens small batches
+  // (single-shot latency) but buys ~1% at full chunks, where every kernel already fills the
+  // chip and the overlap only stretches each kernel's span (profiles/r2/ab_streams*.json).
+  const bool fork = ctx->streams == 2 || (ctx->streams == 0 && chunk < QRK_FORK_MAX);
+  S.aux = fork ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
@@ -662,7 +670,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
 }
 
 int qrk_ctx_set_streams(qrk_ctx* ctx, int streams) {
-  if (!ctx || streams < 1 || streams > 2) return fail("streams must be 1 or 2");
+  if (!ctx || streams < 0 || streams > 2) return fail("streams must be 0 (auto), 1 or 2");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->streams = streams;
   return 0;

@@ -28,6 +28,11 @@
 namespace qrk {
 namespace mlkem {
 
+// canon_f: add q to negative residues with a sign mask (1) or let the compiler select (0)
+#ifndef QRK_CANON_MASK
+#define QRK_CANON_MASK 1
+#endif
+
 constexpr int Q = 3329;
 constexpr int QINV = 62209;  // q^-1 mod 2^16
 constexpr int XOF_W = 64;    // 256 int16 sampled coefficients (512 B) per matrix entry
@@ -83,6 +88,14 @@ __constant__ TablesF TABFD = make_tables_f();
 constexpr float INV128F = (float)centered(3303);  // 128^-1 mod q (plain domain)
 
 // ---------------------------------------------------------------- arithmetic
+// x < 0 ? -1 : 0 as one v_ashrrev_i32 (inline asm, so the compiler keeps the mask arithmetic
+// instead of turning it back into v_cmp + v_cndmask_e64, whose SGPR lane mask costs a VOP3
+// issue and hazard wait states)
+__device__ __forceinline__ int sign_mask(int x) {
+  int r;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // Signed Montgomery reduction, R = 2^16: returns a * R^-1 mod q, |r| < 2^15 + q/2.
 // 4 full-rate VALU ops: v_mul_u32_u24, v_bfe_i32, v_mad_i32_i24, v_ashrrev.
 __device__ __forceinline__ int mont_reduce(int a) {
@@ -131,7 +144,11 @@ __device__ __forceinline__ uint32_t f2bits(float x) {  // low 16 bits = x as int
 // canonical [0, q) integer of an exact fp32 integer
 __device__ __forceinline__ int canon_f(float x) {
   const int r = f2i(reduce_f(x));
+#if QRK_CANON_MASK
+  return r + (sign_mask(r) & Q);
+#else
   return r + ((r >> 31) & Q);
+#endif
 }
 // basemul accumulator (|acc| < 2^31) -> centered residue: acc = hi 2^16 + lo with
 // 2^16 = -1044 (mod q), |hi * 1044 + lo| < 5.1e6 (exact), then one reduction
@@ -232,14 +249,6 @@ __device__ __forceinline__ uint32_t and_or3(uint32_t a, uint32_t m, uint32_t b) 
 __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
   uint32_t r;
   asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
-  return r;
-}
-
-// x < 0 ? -1 : 0 as one v_ashrrev_i32 (inline asm, so the compiler keeps the mask arithmetic
-// instead of turning it back into v_cmp + v_cndmask)
-__device__ __forceinline__ int sign_mask(int x) {
-  int r;
-  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
   return r;
 }
 
@@ -977,11 +986,24 @@ __device__ __forceinline__ PK8 decode12(const uint8_t* __restrict__ src, bool& b
   split12((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, v);
   split12((uint32_t)(b >> 32), (uint32_t)c, (uint32_t)(c >> 32), v + 8);
   PK8 r;
+#if QRK_CANON_MASK
+  // unsigned min(v, v - q) is v mod q for v < 2q (v - q wraps when v < q); the largest
+  // coefficient decides the modulus check (two full-rate ops and one max, no lane masks)
+  uint32_t mx = 0;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const uint32_t u = (uint32_t)v[t];
+    mx = u > mx ? u : mx;
+    v[t] = (int)__builtin_elementwise_min(u, u - (uint32_t)Q);
+  }
+  bad |= mx >= (uint32_t)Q;
+#else
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     bad |= v[t] >= Q;
     v[t] = v[t] >= Q ? v[t] - Q : v[t];
   }
+#endif
 #pragma unroll
   for (int u = 0; u < 8; ++u) r.w[u] = pack16(v[2 * u], v[2 * u + 1]);
   return r;

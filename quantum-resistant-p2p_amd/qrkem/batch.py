@@ -192,7 +192,8 @@ class BatchKEM:
         return int(LIB.qrk_ctx_effective_chunk(self._ctx, self.alg.encode()))
 
     def set_streams(self, streams: int) -> None:
-        """2: fork independent kernel chains onto a side stream (default); 1: serial."""
+        """0: auto (fork below 65536 handshakes per chunk, the default); 2: always fork independent
+        kernel chains onto a side stream; 1: always serial."""
         self._check(LIB.qrk_ctx_set_streams(self._ctx, streams), "set_streams")
 
     # ------------------------------------------------------------------ kernel timing
