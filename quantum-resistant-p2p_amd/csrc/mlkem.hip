@@ -302,6 +302,31 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 // FIX == true: one lane per listed entry recomputes it with as many blocks as
 // it needs (rewriting identical chunks), so the rare 4th block never idles a
 // whole wave.
+// One SampleNTT entry inst = (x K + y) C + hs: SHAKE128(rho || x || y), ALL = false: exactly 3
+// blocks (returns the count, < 256 when a 4th block is needed); ALL = true: as many blocks as it
+// takes.  rb = this lane's ring column (see compact_block).
+template <int K, bool ALL>
+__device__ __forceinline__ int xof_entry(const uint8_t* __restrict__ rho_base, size_t rho_stride, size_t C,
+                                         size_t inst, uint4* __restrict__ out, char* ring_all, uint32_t rb) {
+  const size_t hs = inst % C;
+  const int xy = (int)(inst / C);
+  uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
+  const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
+  KState s;
+  kzero(s);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
+  s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
+  s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
+  int cnt = 0;
+#pragma unroll 1
+  for (int b = 0; b < (ALL ? MAX_XOF_BLOCKS : 3) && (!ALL || cnt < 256); ++b) {
+    keccak_f(s);
+    compact_block(s, ring_all, rb, cnt, dst);
+  }
+  return cnt;
+}
+
 template <int K, bool FIX>
 __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
                                              size_t n, size_t C, uint4* __restrict__ out,
@@ -314,23 +339,8 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 #pragma unroll 1
   for (; r < limit; r += stride) {
     const size_t inst = FIX ? (size_t)fix[r] : r;
-    const size_t hs = inst % C;
-    const int xy = (int)(inst / C);
-    if (!FIX && hs >= n) return;
-    uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
-    const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
-    KState s;
-    kzero(s);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
-    s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
-    s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
-    int cnt = 0;
-#pragma unroll 1
-    for (int b = 0; b < (FIX ? MAX_XOF_BLOCKS : 3) && (!FIX || cnt < 256); ++b) {
-      keccak_f(s);
-      compact_block(s, (char*)ring_all, rb, cnt, dst);
-    }
+    if (!FIX && inst % C >= n) return;
+    const int cnt = xof_entry<K, FIX>(rho_base, rho_stride, C, inst, out, (char*)ring_all, rb);
     if (!FIX) {
       if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
       return;
@@ -341,13 +351,10 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 // PRF producer: SHAKE256(seed || N) -> 64*eta bytes; inst = N * C + hs.
 // eta = (N < eta1_upto) ? ETA1 : ETA2.
 template <int ETA1, int ETA2>
-__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
-                                             int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
-  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (inst >= (size_t)nprf * C) return;
+__device__ __forceinline__ void prf_inst(const uint64_t* __restrict__ seeds, size_t C, size_t inst, int eta1_upto,
+                                         uint64_t* __restrict__ prf) {
   const size_t hs = inst % C;
   const int N = (int)(inst / C);
-  if (hs >= n) return;
   const int eta = N < eta1_upto ? ETA1 : ETA2;
   KState s;
   kzero(s);
@@ -368,6 +375,14 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __rest
   }
 }
 
+template <int ETA1, int ETA2>
+__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
+                                             int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
+  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (inst >= (size_t)nprf * C || inst % C >= n) return;
+  prf_inst<ETA1, ETA2>(seeds, C, inst, eta1_upto, prf);
+}
+
 template <int K>
 struct P {
   static constexpr int ETA1 = (K == 2) ? 3 : 2;
@@ -381,11 +396,8 @@ struct P {
 
 // KeyGen front: (rho, sigma) = G(d || k).  rho -> pk[384k..] and dk's ek copy; sigma -> seeds.
 template <int K>
-__global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict__ coins, size_t n,
-                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
-                                                      uint64_t* __restrict__ seeds) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
+__device__ __forceinline__ void front_keygen_hs(const uint8_t* __restrict__ coins, size_t hs, uint8_t* __restrict__ pk,
+                                                uint8_t* __restrict__ sk, uint64_t* __restrict__ seeds) {
   const uint64_t* d = (const uint64_t*)(coins + hs * 64);
   KState s;
   kzero(s);
@@ -403,13 +415,18 @@ __global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict_
     seeds[hs * 4 + w] = kword(s, 4 + w);
   }
 }
+template <int K>
+__global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict__ coins, size_t n,
+                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                      uint64_t* __restrict__ seeds) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs < n) front_keygen_hs<K>(coins, hs, pk, sk, seeds);
+}
 
 // KeyGen back: dk = dk_pke || ek || H(ek) || z  (ek already copied by the core kernel)
 template <int K>
-__global__ __launch_bounds__(256) void k_back_keygen(const uint8_t* __restrict__ coins, size_t n,
-                                                     const uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
+__device__ __forceinline__ void back_keygen_hs(const uint8_t* __restrict__ coins, size_t hs,
+                                               const uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
   const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
   KState s;
   kzero(s);
@@ -422,14 +439,17 @@ __global__ __launch_bounds__(256) void k_back_keygen(const uint8_t* __restrict__
     tail[4 + w] = z[w];
   }
 }
+template <int K>
+__global__ __launch_bounds__(256) void k_back_keygen(const uint8_t* __restrict__ coins, size_t n,
+                                                     const uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs < n) back_keygen_hs<K>(coins, hs, pk, sk);
+}
 
 // Encaps front: (K, r) = G(m || H(ek)); K -> ss, r -> seeds
 template <int K>
-__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_encaps(const uint8_t* __restrict__ pk,
-                                                      const uint8_t* __restrict__ coins, size_t n,
-                                                      uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
+__device__ __forceinline__ void front_encaps_hs(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ coins,
+                                                size_t hs, uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
   const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
   KState s;
   kzero(s);
@@ -447,18 +467,19 @@ __global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_encaps(const uint8
     seeds[hs * 4 + w] = kword(s, 4 + w);
   }
 }
+template <int K>
+__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_encaps(const uint8_t* __restrict__ pk,
+                                                      const uint8_t* __restrict__ coins, size_t n,
+                                                      uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs < n) front_encaps_hs<K>(pk, coins, hs, ss, seeds);
+}
 
 // Decaps front: (K', r') = G(m' || h), Kbar = J(z || c)
 template <int K>
-__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8_t* __restrict__ ct,
-                                                      const uint8_t* __restrict__ sk,
-                                                      const uint64_t* __restrict__ mprime, size_t n,
-                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
-                                                      uint64_t* __restrict__ kbar) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
+__device__ __forceinline__ void g_decaps_hs(const uint8_t* __restrict__ sk, const uint64_t* __restrict__ mprime,
+                                            size_t hs, uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime) {
   const uint64_t* h = (const uint64_t*)(sk + hs * P<K>::SK + 768 * K + 32);
-  const uint64_t* z = h + 4;
   const uint64_t* m = mprime + hs * 4;
   KState s;
   kzero(s);
@@ -468,11 +489,28 @@ __global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8
     kprime[hs * 4 + w] = kword(s, w);
     seeds[hs * 4 + w] = kword(s, 4 + w);
   }
+}
+template <int K>
+__device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk, size_t hs,
+                                            uint64_t* __restrict__ kbar) {
+  const uint64_t* z = (const uint64_t*)(sk + hs * P<K>::SK + 768 * K + 64);
   const uint64_t* c = (const uint64_t*)(ct + hs * P<K>::CT);
+  KState s;
   kzero(s);
   absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
+}
+template <int K>
+__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk,
+                                                      const uint64_t* __restrict__ mprime, size_t n,
+                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
+                                                      uint64_t* __restrict__ kbar) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
+  j_decaps_hs<K>(ct, sk, hs, kbar);
 }
 
 // ============================================================ 16-lane polynomial groups
@@ -1064,13 +1102,9 @@ inline ScratchView carve(void* base, int K, size_t C) {
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
 template <int K>
-__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
-                                                     uint8_t* __restrict__ sk) {
-  __shared__ GroupLds lds[GROUPS];
-  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  GroupLds& g = lds[gi];
-  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
+                                                     uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
   uint8_t* ek = pk + hs * P<K>::PK;
@@ -1124,23 +1158,27 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
     }
   }
 }
+template <int K>
+__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+                                                     const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
+                                                     uint8_t* __restrict__ sk) {
+  __shared__ GroupLds lds[GROUPS];
+  const int gi = threadIdx.x >> 4;
+  keygen_core_hs<K>(n, C, xof, prf, pk, sk, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+}
 
 // ------------------------------------------------------------ K-PKE.Encrypt core
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
 template <int K, int MODE>
-__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
                                                       uint8_t* __restrict__ ct, int32_t* __restrict__ status,
                                                       const uint64_t* __restrict__ kprime,
-                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
+                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
-  __shared__ GroupLds lds[GROUPS];
-  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  GroupLds& g = lds[gi];
-  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
   const uint8_t* ek = ek_base + hs * ek_stride;
@@ -1252,16 +1290,24 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
     }
   }
 }
+template <int K, int MODE>
+__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+                                                      const uint64_t* __restrict__ prf,
+                                                      const uint8_t* __restrict__ ek_base, size_t ek_stride,
+                                                      const uint8_t* __restrict__ m_base, size_t m_stride,
+                                                      uint8_t* __restrict__ ct, int32_t* __restrict__ status,
+                                                      const uint64_t* __restrict__ kprime,
+                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
+  __shared__ GroupLds lds[GROUPS];
+  const int gi = threadIdx.x >> 4;
+  encrypt_core_hs<K, MODE>(n, C, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+}
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K>
-__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
-                                                      const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
+__device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
-  __shared__ GroupLds lds[GROUPS];
-  const int L = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  GroupLds& g = lds[gi];
-  const size_t hs_raw = (size_t)blockIdx.x * GROUPS + gi;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
   const uint8_t* c = ct + hs * P<K>::CT;
@@ -1295,6 +1341,106 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
     bits |= (uint32_t)compress<1>(x) << t;
   }
   if (active) ((uint16_t*)(mprime + hs * 4))[L] = (uint16_t)bits;
+}
+template <int K>
+__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
+  __shared__ GroupLds lds[GROUPS];
+  const int gi = threadIdx.x >> 4;
+  decrypt_core_hs<K>(n, ct, sk, mprime, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+}
+
+// ============================================================ small batches: one launch per operation
+// The reference calls one KeyGen / Encaps / Decaps at a time (key_exchange.py:133, 156, 179):
+// there the batched schedule's per-kernel launches and drains dominate.  For small n one
+// workgroup per handshake runs the whole operation in a single launch: the long sponge chain on
+// one lane (H(ek) + G, or J(z || c)), the SampleNTT entries on the lanes of another wave at the
+// same time, the PRFs right after G, then the 16-lane polynomial group.  Intermediates use the
+// same scratch layouts as the batched kernels (C = chunk rounded to 64).
+#ifndef QRK_SMALL_MAX
+#define QRK_SMALL_MAX 256
+#endif
+// ordering between lanes of one wave across phases (global scratch written by one lane, read by
+// others): a workgroup-scope release / acquire around a wave barrier
+__device__ __forceinline__ void wave_phase() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_encaps_small(size_t n, size_t C, const uint8_t* __restrict__ pk,
+                                                      const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
+                                                      uint8_t* __restrict__ ss, int32_t* __restrict__ status,
+                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
+                                                      uint64_t* __restrict__ seeds) {
+  __shared__ uint32_t ring_all[4 * 16 * 64];
+  __shared__ GroupLds g;
+  const size_t hs = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 0) {
+    if (lane == 0) front_encaps_hs<K>(pk, coins, hs, ss, seeds);  // H(ek), G: the critical chain
+    wave_phase();
+    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2>(seeds, C, (size_t)lane * C + hs, K, prf);
+  } else if (wave == 1 && lane < K * K) {
+    xof_entry<K, true>(pk + 384 * K, (size_t)P<K>::PK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
+                       (uint32_t)(16 * 64 + lane) * 4);
+  }
+  __syncthreads();
+  if (threadIdx.x < 16)
+    encrypt_core_hs<K, 0>(n, C, xof, prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
+                          nullptr, hs, (int)threadIdx.x, g);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_decaps_small(size_t n, size_t C, const uint8_t* __restrict__ ct,
+                                                      const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss,
+                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
+                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ mprime,
+                                                      uint64_t* __restrict__ kprime, uint64_t* __restrict__ kbar) {
+  __shared__ uint32_t ring_all[4 * 16 * 64];
+  __shared__ GroupLds g;
+  const size_t hs = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave == 0) {  // m' = Decrypt, (K', r') = G(m' || h), PRF(r')
+    if (lane < 16) decrypt_core_hs<K>(n, ct, sk, mprime, hs, lane, g);
+    wave_phase();
+    if (lane == 0) g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
+    wave_phase();
+    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2>(seeds, C, (size_t)lane * C + hs, K, prf);
+  } else if (wave == 1) {  // Kbar = J(z || c) beside it
+    if (lane == 0) j_decaps_hs<K>(ct, sk, hs, kbar);
+  } else if (wave == 2 && lane < K * K) {
+    xof_entry<K, true>(sk + 768 * K, (size_t)P<K>::SK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
+                       (uint32_t)(2 * 16 * 64 + lane) * 4);
+  }
+  __syncthreads();
+  if (threadIdx.x < 16)
+    encrypt_core_hs<K, 1>(n, C, xof, prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)mprime, (size_t)32,
+                          const_cast<uint8_t*>(ct), (int32_t*)nullptr, kprime, kbar, ss, hs, (int)threadIdx.x, g);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_keygen_small(size_t n, size_t C, const uint8_t* __restrict__ coins,
+                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
+                                                      uint64_t* __restrict__ seeds) {
+  __shared__ uint32_t ring_all[4 * 16 * 64];
+  __shared__ GroupLds g;
+  const size_t hs = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) front_keygen_hs<K>(coins, hs, pk, sk, seeds);  // (rho, sigma) = G(d || k)
+  __syncthreads();
+  if (wave == 0 && lane < 2 * K) {
+    prf_inst<P<K>::ETA1, P<K>::ETA1>(seeds, C, (size_t)lane * C + hs, 2 * K, prf);
+  } else if (wave == 1 && lane < K * K) {
+    xof_entry<K, true>(pk + 384 * K, (size_t)P<K>::PK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
+                       (uint32_t)(16 * 64 + lane) * 4);
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) keygen_core_hs<K>(n, C, xof, prf, pk, sk, hs, (int)threadIdx.x, g);
+  __syncthreads();
+  if (threadIdx.x == 0) back_keygen_hs<K>(coins, hs, pk, sk);  // H(ek) of the finished ek
 }
 
 // ============================================================ host launchers
@@ -1335,6 +1481,11 @@ template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
+  if (n <= QRK_SMALL_MAX) {
+    QRK_LAUNCH("k_keygen_small", s.main, k_keygen_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, coins, pk,
+               sk, v.xof, v.prf, v.seeds);
+    return hipGetLastError();
+  }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds);
@@ -1354,6 +1505,11 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
                        int32_t* status, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
+  if (n <= QRK_SMALL_MAX) {
+    QRK_LAUNCH("k_encaps_small", s.main, k_encaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, pk, coins,
+               ct, ss, status, v.xof, v.prf, v.seeds);
+    return hipGetLastError();
+  }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   fork(s);
   launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd);
@@ -1373,6 +1529,11 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
                        const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
+  if (n <= QRK_SMALL_MAX) {
+    QRK_LAUNCH("k_decaps_small", s.main, k_decaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, ct, sk, ss,
+               v.xof, v.prf, v.seeds, v.mprime, v.kprime, v.kbar);
+    return hipGetLastError();
+  }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   fork(s);
