@@ -167,8 +167,11 @@ __device__ __forceinline__ int decompress(int y) {
   return (int)(((uint32_t)Q * (uint32_t)y + (1u << (D - 1))) >> D);
 }
 
+// Tiled scratch layouts: word w of instance i at ((i / TW) W + w) TW + i % TW -- TW = 64 for the
+// batched kernels (one coalesced wave store per word), 16 for the small path's LDS copies.
+template <int TW = 64>
 __device__ __forceinline__ size_t tidx(size_t inst, int w, int W) {
-  return ((inst >> 6) * (size_t)W + (size_t)w) * 64 + (inst & 63);
+  return ((inst / TW) * (size_t)W + (size_t)w) * TW + (inst % TW);
 }
 
 // 16-lane group synchronisation: a group never spans two waves, so ordering
@@ -257,6 +260,7 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 // `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
 // 8-11 are zero, so an entry address is one v_bitop3_b32, (pos & 0xF00) | rb, with the static
 // LDS base folded into the ds_write offset.
+template <int TW = 64>
 __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
 #pragma unroll
@@ -292,7 +296,7 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 64], 16, r[(2 * j) * 64]);
-      dst[ch * 64] = make_uint4(w[0], w[1], w[2], w[3]);
+      dst[ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
@@ -305,13 +309,10 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 // One SampleNTT entry inst = (x K + y) C + hs: SHAKE128(rho || x || y), ALL = false: exactly 3
 // blocks (returns the count, < 256 when a 4th block is needed); ALL = true: as many blocks as it
 // takes.  rb = this lane's ring column (see compact_block).
-template <int K, bool ALL>
-__device__ __forceinline__ int xof_entry(const uint8_t* __restrict__ rho_base, size_t rho_stride, size_t C,
-                                         size_t inst, uint4* __restrict__ out, char* ring_all, uint32_t rb) {
-  const size_t hs = inst % C;
-  const int xy = (int)(inst / C);
-  uint4* dst = out + (inst >> 6) * 32 * 64 + (inst & 63);
-  const uint64_t* rho = (const uint64_t*)(rho_base + hs * rho_stride);
+template <int K, bool ALL, int TW = 64>
+__device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, uint4* __restrict__ out,
+                                         char* ring_all, uint32_t rb) {
+  uint4* dst = out + (inst / TW) * 32 * TW + (inst % TW);
   KState s;
   kzero(s);
 #pragma unroll
@@ -322,7 +323,7 @@ __device__ __forceinline__ int xof_entry(const uint8_t* __restrict__ rho_base, s
 #pragma unroll 1
   for (int b = 0; b < (ALL ? MAX_XOF_BLOCKS : 3) && (!ALL || cnt < 256); ++b) {
     keccak_f(s);
-    compact_block(s, ring_all, rb, cnt, dst);
+    compact_block<TW>(s, ring_all, rb, cnt, dst);
   }
   return cnt;
 }
@@ -340,7 +341,8 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
   for (; r < limit; r += stride) {
     const size_t inst = FIX ? (size_t)fix[r] : r;
     if (!FIX && inst % C >= n) return;
-    const int cnt = xof_entry<K, FIX>(rho_base, rho_stride, C, inst, out, (char*)ring_all, rb);
+    const int cnt = xof_entry<K, FIX>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst,
+                                      out, (char*)ring_all, rb);
     if (!FIX) {
       if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
       return;
@@ -350,28 +352,26 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 
 // PRF producer: SHAKE256(seed || N) -> 64*eta bytes; inst = N * C + hs.
 // eta = (N < eta1_upto) ? ETA1 : ETA2.
-template <int ETA1, int ETA2>
-__device__ __forceinline__ void prf_inst(const uint64_t* __restrict__ seeds, size_t C, size_t inst, int eta1_upto,
+template <int ETA1, int ETA2, int TW = 64>
+__device__ __forceinline__ void prf_inst(const uint64_t* __restrict__ seed, int N, size_t inst, int eta1_upto,
                                          uint64_t* __restrict__ prf) {
-  const size_t hs = inst % C;
-  const int N = (int)(inst / C);
   const int eta = N < eta1_upto ? ETA1 : ETA2;
   KState s;
   kzero(s);
 #pragma unroll
-  for (int w = 0; w < 4; ++w) kxor(s, w, seeds[hs * 4 + w]);
+  for (int w = 0; w < 4; ++w) kxor(s, w, seed[w]);
   s.a[4].lo ^= (uint32_t)N | (DS_SHAKE << 8);
   s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
   keccak_f(s);
   if (eta == 2) {
 #pragma unroll
-    for (int w = 0; w < 16; ++w) prf[tidx(inst, w, PRF_W)] = kword(s, w);
+    for (int w = 0; w < 16; ++w) prf[tidx<TW>(inst, w, PRF_W)] = kword(s, w);
   } else {
 #pragma unroll
-    for (int w = 0; w < 17; ++w) prf[tidx(inst, w, PRF_W)] = kword(s, w);
+    for (int w = 0; w < 17; ++w) prf[tidx<TW>(inst, w, PRF_W)] = kword(s, w);
     keccak_f(s);
 #pragma unroll
-    for (int w = 0; w < 7; ++w) prf[tidx(inst, 17 + w, PRF_W)] = kword(s, w);
+    for (int w = 0; w < 7; ++w) prf[tidx<TW>(inst, 17 + w, PRF_W)] = kword(s, w);
   }
 }
 
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __rest
                                              int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
   const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (inst >= (size_t)nprf * C || inst % C >= n) return;
-  prf_inst<ETA1, ETA2>(seeds, C, inst, eta1_upto, prf);
+  prf_inst<ETA1, ETA2>(seeds + (inst % C) * 4, (int)(inst / C), inst, eta1_upto, prf);
 }
 
 template <int K>
@@ -858,15 +858,15 @@ __device__ __forceinline__ void basemul_acc(int acc[16], const PK8& a, const BOp
 struct CbdRaw {
   uint32_t d[3];
 };
-template <int ETA>
+template <int ETA, int TW = 64>
 __device__ __forceinline__ CbdRaw cbd_load(const uint64_t* __restrict__ prf, size_t inst, int L) {
   CbdRaw r;
   if constexpr (ETA == 2) {
-    const uint64_t w = prf[tidx(inst, L, PRF_W)];
+    const uint64_t w = prf[tidx<TW>(inst, L, PRF_W)];
     r.d[0] = (uint32_t)w, r.d[1] = (uint32_t)(w >> 32), r.d[2] = 0;
   } else {
     const int wi = (3 * L) >> 1;
-    const uint64_t a = prf[tidx(inst, wi, PRF_W)], b = prf[tidx(inst, wi + 1, PRF_W)];
+    const uint64_t a = prf[tidx<TW>(inst, wi, PRF_W)], b = prf[tidx<TW>(inst, wi + 1, PRF_W)];
     const bool odd = L & 1;
     r.d[0] = odd ? (uint32_t)(a >> 32) : (uint32_t)a;
     r.d[1] = odd ? (uint32_t)b : (uint32_t)(a >> 32);
@@ -1009,9 +1009,10 @@ __device__ __forceinline__ void flush_cmp(GroupLds& g, const CmpWords<D>& c, uin
 
 // SampleNTT consumer: lane L loads coefficients 16L..16L+15 (chunks 2L, 2L+1)
 // of the producer's compacted output -- contiguous layout, no parsing.
+template <int TW = 64>
 __device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t inst, int L) {
-  const uint4* base = xs + (inst >> 6) * 32 * 64 + (inst & 63);
-  const uint4 u = base[(2 * L) * 64], v = base[(2 * L + 1) * 64];
+  const uint4* base = xs + (inst / TW) * 32 * TW + (inst % TW);
+  const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
   return PK8{{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}};
 }
 
@@ -1101,19 +1102,20 @@ inline ScratchView carve(void* base, int K, size_t C) {
 // ------------------------------------------------------------ KeyGen core
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
-template <int K>
+template <int K, int TW = 64>
 __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
+  const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   BOp sb[K];
   {
     CbdRaw sr[K];  // every s_j's CBD words issued before the first NTT
 #pragma unroll
-    for (int j = 0; j < K; ++j) sr[j] = cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L);
+    for (int j = 0; j < K; ++j) sr[j] = cbd_load<P<K>::ETA1, TW>(prf, (size_t)j * C + hss, L);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       PF16 f;
@@ -1130,8 +1132,8 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)(j * K) * C + hs, L);
-  CbdRaw er = cbd_load<P<K>::ETA1>(prf, (size_t)K * C + hs, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)(j * K) * C + hss, L);
+  CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
@@ -1142,8 +1144,8 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)(j * K + i + 1) * C + hs, L);
-      er = cbd_load<P<K>::ETA1>(prf, (size_t)(K + i + 1) * C + hs, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)(j * K + i + 1) * C + hss, L);
+      er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
     }
     PF16 ef;
     cbd_f<P<K>::ETA1>(ef, ecur);
@@ -1170,7 +1172,7 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
 // ------------------------------------------------------------ K-PKE.Encrypt core
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
-template <int K, int MODE>
+template <int K, int MODE, int TW = 64>
 __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
@@ -1181,6 +1183,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
+  const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
@@ -1189,7 +1192,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   {
     CbdRaw yr[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) yr[j] = cbd_load<P<K>::ETA1>(prf, (size_t)j * C + hs, L);
+    for (int j = 0; j < K; ++j) yr[j] = cbd_load<P<K>::ETA1, TW>(prf, (size_t)j * C + hss, L);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       PF16 f;
@@ -1206,9 +1209,9 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 #if QRK_ENC_PREFETCH
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)j * C + hs, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)j * C + hss, L);
 #endif
-  CbdRaw er = cbd_load<P<K>::ETA2>(prf, (size_t)K * C + hs, L);
+  CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
@@ -1219,16 +1222,16 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
 #else
 #pragma unroll
-    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled((const uint4*)xof, (size_t)(i * K + j) * C + hs, L), yb[j]);
+    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW>((const uint4*)xof, (size_t)(i * K + j) * C + hss, L), yb[j]);
 #endif
     const CbdRaw ecur = er;
 #if QRK_ENC_PREFETCH
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hs, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hss, L);
     }
 #endif
-    er = cbd_load<P<K>::ETA2>(prf, (size_t)(K + i + 1) * C + hs, L);  // e1_{i+1}, or e2 after the last row
+    er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
     PF16 uf;
 #pragma unroll
     for (int t = 0; t < 16; ++t) uf.v[t] = acc_to_f(acc[t]);
@@ -1368,77 +1371,80 @@ __device__ __forceinline__ void wave_phase() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// LDS copies of one handshake's SampleNTT entries and PRF outputs (tile width 16, C = 1)
+struct SmallLds {
+  uint32_t ring[16 * 64];  // one wave's compaction rings
+  uint4 xs[32 * 16];       // chunk c of entry e at c * 16 + e (K^2 <= 16 entries)
+  uint64_t ps[PRF_W * 16]; // word w of PRF instance N at w * 16 + N (2K + 1 <= 9)
+  GroupLds g;
+};
+
 template <int K>
-__global__ __launch_bounds__(256) void k_encaps_small(size_t n, size_t C, const uint8_t* __restrict__ pk,
+__global__ __launch_bounds__(256) void k_encaps_small(size_t n, const uint8_t* __restrict__ pk,
                                                       const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
                                                       uint8_t* __restrict__ ss, int32_t* __restrict__ status,
-                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
                                                       uint64_t* __restrict__ seeds) {
-  __shared__ uint32_t ring_all[4 * 16 * 64];
-  __shared__ GroupLds g;
+  __shared__ __attribute__((aligned(16))) SmallLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave == 0) {
     if (lane == 0) front_encaps_hs<K>(pk, coins, hs, ss, seeds);  // H(ek), G: the critical chain
     wave_phase();
-    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2>(seeds, C, (size_t)lane * C + hs, K, prf);
+    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2, 16>(seeds + hs * 4, lane, (size_t)lane, K, sl.ps);
   } else if (wave == 1 && lane < K * K) {
-    xof_entry<K, true>(pk + 384 * K, (size_t)P<K>::PK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
-                       (uint32_t)(16 * 64 + lane) * 4);
+    xof_entry<K, true, 16>((const uint64_t*)(pk + hs * P<K>::PK + 384 * K), lane, (size_t)lane, sl.xs,
+                           (char*)sl.ring, (uint32_t)lane * 4);
   }
   __syncthreads();
   if (threadIdx.x < 16)
-    encrypt_core_hs<K, 0>(n, C, xof, prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
-                          nullptr, hs, (int)threadIdx.x, g);
+    encrypt_core_hs<K, 0, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
+                              nullptr, nullptr, nullptr, hs, (int)threadIdx.x, sl.g);
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void k_decaps_small(size_t n, size_t C, const uint8_t* __restrict__ ct,
+__global__ __launch_bounds__(256) void k_decaps_small(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss,
-                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
                                                       uint64_t* __restrict__ seeds, uint64_t* __restrict__ mprime,
                                                       uint64_t* __restrict__ kprime, uint64_t* __restrict__ kbar) {
-  __shared__ uint32_t ring_all[4 * 16 * 64];
-  __shared__ GroupLds g;
+  __shared__ __attribute__((aligned(16))) SmallLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave == 0) {  // m' = Decrypt, (K', r') = G(m' || h), PRF(r')
-    if (lane < 16) decrypt_core_hs<K>(n, ct, sk, mprime, hs, lane, g);
+    if (lane < 16) decrypt_core_hs<K>(n, ct, sk, mprime, hs, lane, sl.g);
     wave_phase();
     if (lane == 0) g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
     wave_phase();
-    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2>(seeds, C, (size_t)lane * C + hs, K, prf);
+    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2, 16>(seeds + hs * 4, lane, (size_t)lane, K, sl.ps);
   } else if (wave == 1) {  // Kbar = J(z || c) beside it
     if (lane == 0) j_decaps_hs<K>(ct, sk, hs, kbar);
   } else if (wave == 2 && lane < K * K) {
-    xof_entry<K, true>(sk + 768 * K, (size_t)P<K>::SK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
-                       (uint32_t)(2 * 16 * 64 + lane) * 4);
+    xof_entry<K, true, 16>((const uint64_t*)(sk + hs * P<K>::SK + 768 * K), lane, (size_t)lane, sl.xs,
+                           (char*)sl.ring, (uint32_t)lane * 4);
   }
   __syncthreads();
   if (threadIdx.x < 16)
-    encrypt_core_hs<K, 1>(n, C, xof, prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)mprime, (size_t)32,
-                          const_cast<uint8_t*>(ct), (int32_t*)nullptr, kprime, kbar, ss, hs, (int)threadIdx.x, g);
+    encrypt_core_hs<K, 1, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, sk + 384 * K, (size_t)P<K>::SK,
+                              (const uint8_t*)mprime, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, kprime,
+                              kbar, ss, hs, (int)threadIdx.x, sl.g);
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void k_keygen_small(size_t n, size_t C, const uint8_t* __restrict__ coins,
+__global__ __launch_bounds__(256) void k_keygen_small(size_t n, const uint8_t* __restrict__ coins,
                                                       uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
-                                                      uint64_t* __restrict__ xof, uint64_t* __restrict__ prf,
                                                       uint64_t* __restrict__ seeds) {
-  __shared__ uint32_t ring_all[4 * 16 * 64];
-  __shared__ GroupLds g;
+  __shared__ __attribute__((aligned(16))) SmallLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (threadIdx.x == 0) front_keygen_hs<K>(coins, hs, pk, sk, seeds);  // (rho, sigma) = G(d || k)
   __syncthreads();
   if (wave == 0 && lane < 2 * K) {
-    prf_inst<P<K>::ETA1, P<K>::ETA1>(seeds, C, (size_t)lane * C + hs, 2 * K, prf);
+    prf_inst<P<K>::ETA1, P<K>::ETA1, 16>(seeds + hs * 4, lane, (size_t)lane, 2 * K, sl.ps);
   } else if (wave == 1 && lane < K * K) {
-    xof_entry<K, true>(pk + 384 * K, (size_t)P<K>::PK, C, (size_t)lane * C + hs, (uint4*)xof, (char*)ring_all,
-                       (uint32_t)(16 * 64 + lane) * 4);
+    xof_entry<K, true, 16>((const uint64_t*)(pk + hs * P<K>::PK + 384 * K), lane, (size_t)lane, sl.xs,
+                           (char*)sl.ring, (uint32_t)lane * 4);
   }
   __syncthreads();
-  if (threadIdx.x < 16) keygen_core_hs<K>(n, C, xof, prf, pk, sk, hs, (int)threadIdx.x, g);
+  if (threadIdx.x < 16) keygen_core_hs<K, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, sk, hs, (int)threadIdx.x, sl.g);
   __syncthreads();
   if (threadIdx.x == 0) back_keygen_hs<K>(coins, hs, pk, sk);  // H(ek) of the finished ek
 }
@@ -1482,8 +1488,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_keygen_small", s.main, k_keygen_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, coins, pk,
-               sk, v.xof, v.prf, v.seeds);
+    QRK_LAUNCH("k_keygen_small", s.main, k_keygen_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, coins, pk, sk,
+               v.seeds);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1506,8 +1512,8 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_encaps_small", s.main, k_encaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, pk, coins,
-               ct, ss, status, v.xof, v.prf, v.seeds);
+    QRK_LAUNCH("k_encaps_small", s.main, k_encaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, pk, coins, ct,
+               ss, status, v.seeds);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1530,8 +1536,8 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_decaps_small", s.main, k_decaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, C, ct, sk, ss,
-               v.xof, v.prf, v.seeds, v.mprime, v.kprime, v.kbar);
+    QRK_LAUNCH("k_decaps_small", s.main, k_decaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, ct, sk, ss,
+               v.seeds, v.mprime, v.kprime, v.kbar);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
