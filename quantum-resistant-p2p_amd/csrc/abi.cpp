@@ -134,9 +134,11 @@ struct qrk_ctx {
   size_t dio_bytes = 0;
   uint8_t* hio = nullptr;         // ... and their pinned host mirror
   size_t hio_bytes = 0;
+  uint8_t* hio_dev = nullptr;     // device mapping of hio (zero-copy small calls)
   hipStream_t io_stream = nullptr;
   int streams = 0;            // 0: auto (forked below QRK_FORK_MAX per chunk), 1: serial, 2: forked
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
+  hipStream_t last_stream = nullptr;  // ... on this stream
   bool last_valid = false;
   std::mutex mu;
 };
@@ -150,7 +152,7 @@ static int ctx_order(qrk_ctx* ctx, hipStream_t st) {
     hipError_t e = hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail("hipEventCreate(last use)", e);
   }
-  if (ctx->last_valid) {
+  if (ctx->last_valid && ctx->last_stream != st) {  // same stream: already in order
     hipError_t e = hipStreamWaitEvent(st, ctx->ev_last, 0);
     if (e != hipSuccess) return hip_fail("hipStreamWaitEvent(last use)", e);
   }
@@ -165,7 +167,10 @@ struct LastUse {
   qrk_ctx* ctx;
   hipStream_t st;
   ~LastUse() {
-    if (hipEventRecord(ctx->ev_last, st) == hipSuccess) ctx->last_valid = true;
+    if (hipEventRecord(ctx->ev_last, st) == hipSuccess) {
+      ctx->last_valid = true;
+      ctx->last_stream = st;
+    }
   }
 };
 
@@ -401,6 +406,54 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   return 0;
 }
 
+// Zero-copy host call (see run_batch_host): inputs | outputs packed in the pinned mirror, which
+// the kernel addresses through its device mapping.
+static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2,
+                          const uint8_t* i1, const uint8_t* i2, int32_t* status, size_t l_o1, size_t l_o2,
+                          size_t l_i1, size_t l_i2, hipStream_t st) {
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t b_i1 = al(n * l_i1), b_i2 = al(n * l_i2), b_o1 = al(n * l_o1), b_o2 = al(n * l_o2);
+  const size_t b_st = al(n * sizeof(int32_t)), total = b_i1 + b_i2 + b_o1 + b_o2 + b_st;
+  if (ctx->hio_bytes < total) {
+    ctx_quiesce(ctx);
+    if (ctx->hio) OQS_MEM_cleanse(ctx->hio, ctx->hio_bytes);
+    if (grow_pinned(&ctx->hio, &ctx->hio_bytes, total)) return -1;
+    ctx->hio_dev = nullptr;
+  }
+  if (!ctx->hio_dev) {
+    void* d = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&d, ctx->hio, 0);
+    if (e != hipSuccess) return hip_fail("hipHostGetDevicePointer", e);
+    ctx->hio_dev = (uint8_t*)d;
+  }
+  uint8_t* h = ctx->hio;
+  const size_t o_i2 = b_i1, o_o1 = b_i1 + b_i2, o_o2 = o_o1 + b_o1, o_st = o_o2 + b_o2;
+  // inputs (coins the caller did not supply come from the OS CSPRNG)
+  if (l_i1) {
+    if (i1) memcpy(h, i1, n * l_i1);
+    else if (os_random(h, n * l_i1)) return -1;
+  }
+  if (l_i2) {
+    if (i2) memcpy(h + o_i2, i2, n * l_i2);
+    else if (os_random(h + o_i2, n * l_i2)) return -1;
+  }
+  memset(h + o_st, 0, n * sizeof(int32_t));
+  uint8_t* d = ctx->hio_dev;
+  // ML-KEM decapsulation reports no status (implicit rejection): only encapsulation writes it
+  int rc = run_batch(ctx, a, op, n, d + o_o1, l_o2 ? d + o_o2 : nullptr, l_i1 ? d : nullptr, l_i2 ? d + o_i2 : nullptr,
+                     (status && op == Op::ENCAPS) ? (int32_t*)(d + o_st) : nullptr, st);
+  hipError_t e = rc ? hipSuccess : hipStreamSynchronize(st);
+  if (!rc && e != hipSuccess) rc = hip_fail("kernel execution", e);
+  if (!rc) {
+    memcpy(o1, h + o_o1, n * l_o1);
+    if (l_o2) memcpy(o2, h + o_o2, n * l_o2);
+    if (status) memcpy(status, h + o_st, n * sizeof(int32_t));
+  }
+  if (rc) (void)hipStreamSynchronize(st);  // nothing may still read or write the mirror
+  OQS_MEM_cleanse(h, total);  // coins, secret keys and shared secrets do not outlive the call
+  return rc;
+}
+
 // Host-pointer wrapper: stage inputs, run, copy outputs back, synchronise.  The context
 // keeps a device I/O buffer, a pinned host mirror and its own stream, so a call is one
 // packed H2D copy, the kernels, one packed D2H copy and one synchronise (the reference's
@@ -410,10 +463,14 @@ static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   if (n == 0) return 0;
   DeviceGuard device_guard;
   if (device_guard.set(ctx->device)) return -1;
+  // Small ML-KEM batches (one launch per operation, the reference's single-shot calls) run
+  // zero-copy: the kernel reads its inputs from and writes its outputs to the pinned mirror, and
+  // coins are drawn straight into it, so a call is one launch and one synchronise.
+  const bool zc = a.family == Family::MLKEM && n <= mlkem_small_max();
   size_t l_o1, l_o2, l_i1, l_i2;
   switch (op) {
-    case Op::KEYPAIR: l_o1 = a.pk, l_o2 = a.sk, l_i1 = i1 ? a.kp_coins : 0, l_i2 = 0; break;
-    case Op::ENCAPS: l_o1 = a.ct, l_o2 = a.ss, l_i1 = a.pk, l_i2 = i2 ? a.enc_coins : 0; break;
+    case Op::KEYPAIR: l_o1 = a.pk, l_o2 = a.sk, l_i1 = (i1 || zc) ? a.kp_coins : 0, l_i2 = 0; break;
+    case Op::ENCAPS: l_o1 = a.ct, l_o2 = a.ss, l_i1 = a.pk, l_i2 = (i2 || zc) ? a.enc_coins : 0; break;
     default: l_o1 = a.ss, l_o2 = 0, l_i1 = a.ct, l_i2 = a.sk; break;
   }
   const size_t l_st = status ? sizeof(int32_t) : 0;
@@ -427,7 +484,9 @@ static int run_batch_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
     if (e != hipSuccess) return hip_fail("hipStreamCreate(io)", e);
   }
   hipStream_t st = ctx->io_stream;
+  if (zc) return run_small_host(ctx, a, op, n, o1, o2, i1, i2, status, l_o1, l_o2, l_i1, l_i2, st);
   if (grow_device(ctx, (void**)&ctx->dio, &ctx->dio_bytes, in_bytes + out_bytes, st)) return -1;
+  if (ctx->hio_bytes < in_bytes + out_bytes) ctx->hio_dev = nullptr;  // reallocated below
   if (grow_pinned(&ctx->hio, &ctx->hio_bytes, in_bytes + out_bytes)) return -1;
   uint8_t *d_i1 = ctx->dio, *d_i2 = d_i1 + b_i1, *d_o1 = d_i2 + b_i2, *d_o2 = d_o1 + b_o1, *d_st = d_o2 + b_o2;
   uint8_t* h = ctx->hio;

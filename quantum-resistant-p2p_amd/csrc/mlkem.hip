@@ -23,6 +23,7 @@
 #include <algorithm>
 
 #include "keccak.cuh"
+#include "keccak_coop.cuh"
 #include "qrkem_internal.h"
 
 namespace qrk {
@@ -1099,6 +1100,24 @@ inline ScratchView carve(void* base, int K, size_t C) {
   return v;
 }
 
+// ------------------------------------------------------------ single-shot phase trace (tools only)
+// -DQRK_SS_TRACE=1 (a tools/build_variant.sh build): the single-shot kernels stamp the 100 MHz
+// wall clock at phase boundaries into g_ss_trace; qrk_dbg_ss_trace() copies it out.
+#ifndef QRK_SS_TRACE
+#define QRK_SS_TRACE 0
+#endif
+#if QRK_SS_TRACE
+__device__ unsigned long long g_ss_trace[32];
+#define SS_MARK(cond, i)                                      \
+  do {                                                        \
+    if (cond) g_ss_trace[i] = wall_clock64();                 \
+  } while (0)
+#else
+#define SS_MARK(cond, i) \
+  do {                   \
+  } while (0)
+#endif
+
 // ------------------------------------------------------------ KeyGen core
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
@@ -1184,6 +1203,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
+  const size_t hsm = (TW == 64 || MODE == 0) ? hs : 0;  // m', K', Kbar: LDS on the small decaps path
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
@@ -1202,6 +1222,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
       yb[j] = make_bop_f(f, L);
     }
   }
+  SS_MARK(TW == 16 && L == 0, 5);
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
   // QRK_ENC_PREFETCH: row i+1's matrix entries and the next CBD words are loaded one row
   // ahead (latency hidden inside the wave); 0: each entry is loaded as the basemul needs it
@@ -1250,6 +1271,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     else
       flush_bits<DU>(g, c + 32 * DU * i, nullptr, diff, active, L);
   }
+  SS_MARK(TW == 16 && L == 0, 6);
   // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
   {
     int acc[16];
@@ -1267,7 +1289,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     stride_to_contig_f(vf, (float*)g.poly, L);
     PF16 ef;
     cbd_f<P<K>::ETA2>(ef, er);  // e2
-    const uint8_t* m = m_base + hs * m_stride;
+    const uint8_t* m = m_base + hsm * m_stride;
     const uint32_t mb = (uint32_t)m[2 * L] | ((uint32_t)m[2 * L + 1] << 8);
     P16 v;
 #pragma unroll
@@ -1287,11 +1309,12 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     const uint32_t d = group_or(diff);
     const uint32_t mask = (uint32_t)(((uint64_t)d - 1u) >> 32);  // all-ones iff d == 0, no branch
     if (L < 8) {
-      const uint32_t kp = ((const uint32_t*)(kprime + hs * 4))[L];
-      const uint32_t kb = ((const uint32_t*)(kbar + hs * 4))[L];
+      const uint32_t kp = ((const uint32_t*)(kprime + hsm * 4))[L];
+      const uint32_t kb = ((const uint32_t*)(kbar + hsm * 4))[L];
       if (active) ((uint32_t*)(ss + hs * 32))[L] = (kp & mask) | (kb & ~mask);
     }
   }
+  SS_MARK(TW == 16 && L == 0, 7);
 }
 template <int K, int MODE>
 __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
@@ -1307,7 +1330,7 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
 }
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
-template <int K>
+template <int K, int TW = 64>
 __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
@@ -1343,7 +1366,7 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
     const int x = canon_f(i2f(decompress<DV>(v.v[t])) - w.v[t]);
     bits |= (uint32_t)compress<1>(x) << t;
   }
-  if (active) ((uint16_t*)(mprime + hs * 4))[L] = (uint16_t)bits;
+  if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
 }
 template <int K>
 __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
@@ -1355,98 +1378,303 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
 
 // ============================================================ small batches: one launch per operation
 // The reference calls one KeyGen / Encaps / Decaps at a time (key_exchange.py:133, 156, 179):
-// there the batched schedule's per-kernel launches and drains dominate.  For small n one
-// workgroup per handshake runs the whole operation in a single launch: the long sponge chain on
-// one lane (H(ek) + G, or J(z || c)), the SampleNTT entries on the lanes of another wave at the
-// same time, the PRFs right after G, then the 16-lane polynomial group.  Intermediates use the
-// same scratch layouts as the batched kernels (C = chunk rounded to 64).
+// there the batched schedule's per-kernel launches dominate, and one handshake's sponge chain is
+// the critical path.  For small n one 512-thread workgroup per handshake runs the whole operation
+// in a single launch, every sponge wave-cooperative (keccak_coop.cuh, one state per wave):
+//   encaps: wave 0 H(ek) then G(m || h);    waves 1-7 the K^2 SampleNTT entries
+//   decaps: wave 0 Decrypt then G(m' || h); wave 1 J(z || c);  waves 2-7 SampleNTT
+//   keygen: wave 0 G(d || k), then PRFs and SampleNTT over all waves, the core, H(ek)
+// then the 2K+1 (2K) PRFs, one per wave, and the 16-lane polynomial core.  SampleNTT entries, PRF
+// outputs and the decaps intermediates stay in LDS (the batched layouts at tile width 16, C = 1).
 #ifndef QRK_SMALL_MAX
 #define QRK_SMALL_MAX 256
 #endif
-// ordering between lanes of one wave across phases (global scratch written by one lane, read by
-// others): a workgroup-scope release / acquire around a wave barrier
+constexpr int ONE_WAVES = 8;
+
+// ordering between lanes of one wave across phases: a workgroup-scope release / acquire around
+// a wave barrier
 __device__ __forceinline__ void wave_phase() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// LDS copies of one handshake's SampleNTT entries and PRF outputs (tile width 16, C = 1)
-struct SmallLds {
-  uint32_t ring[16 * 64];  // one wave's compaction rings
-  uint4 xs[32 * 16];       // chunk c of entry e at c * 16 + e (K^2 <= 16 entries)
-  uint64_t ps[PRF_W * 16]; // word w of PRF instance N at w * 16 + N (2K + 1 <= 9)
+// One sponge state spread over the wave: this lane's 64-bit word (index Coop::idx).
+struct CState {
+  uint32_t lo = 0, hi = 0;
+};
+__device__ __forceinline__ void cs_xor(CState& s, uint64_t w) {
+  s.lo ^= (uint32_t)w;
+  s.hi ^= (uint32_t)(w >> 32);
+}
+__device__ __forceinline__ uint64_t cs_word(const CState& s) { return ((uint64_t)s.hi << 32) | s.lo; }
+// word w (per lane) of the state, fetched from the lane that holds it
+__device__ __forceinline__ uint64_t cs_get(const CState& s, int w) {
+  const int a = 4 * coop_lane_of(w);
+  return ((uint64_t)bperm(a, s.hi) << 32) | bperm(a, s.lo);
+}
+// the permutation as a call (one copy of the unrolled rounds per kernel, not one per call site)
+__device__ __noinline__ CState kf_coop(CState s, Coop c) {
+  keccak_f_coop(s.lo, s.hi, c);
+  return s;
+}
+
+// Sponge absorb of NW message words ld(0..NW-1) at rate RW, padded with domain byte DS; the
+// lanes holding state words 0..RW-1 each load their word of the next block before the current
+// block's permutation.
+template <int RW, int NW, uint32_t DS, typename Loader>
+__device__ __forceinline__ void coop_absorb(CState& s, const Coop& c, Loader ld) {
+  constexpr int NFULL = NW / RW, TAIL = NW % RW;
+  const int i = c.idx;
+  const bool rl = i >= 0 && i < RW;
+  uint64_t nxt = (rl && (NFULL > 0 || i < TAIL)) ? ld(i) : 0;
+#pragma unroll 1
+  for (int b = 0; b < NFULL; ++b) {
+    cs_xor(s, nxt);
+    nxt = (rl && (b + 1 < NFULL || i < TAIL)) ? ld((b + 1) * RW + i) : 0;
+    s = kf_coop(s, c);
+  }
+  cs_xor(s, nxt);
+  if (i == TAIL) s.lo ^= DS;
+  if (i == RW - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+}
+
+// SampleNTT entry e = x K + y (FIPS 203 Alg. 7) on one wave: SHAKE128(rho || x || y) squeezed
+// block by block; each block's 56 byte triples are parsed by lanes 0-55 (two candidates each)
+// and the accepted ones placed by ballot prefix counts, so the wave keeps FIPS order.  Output:
+// coefficient j of entry e at int16 index ((j / 8) 16 + e) 8 + j % 8 of xs16 (the k_xof layout at
+// tile width 16).  pbuf: this wave's 44-dword LDS parse buffer.
+template <int K>
+__device__ __forceinline__ void xof_coop(const uint64_t* __restrict__ rho, int e, uint16_t* __restrict__ xs16,
+                                         uint32_t* __restrict__ pbuf, const Coop& c) {
+  const int i = c.idx, lane = threadIdx.x & 63;
+  CState s;
+  if (i >= 0 && i < 4) cs_xor(s, rho[i]);
+  if (i == 4) s.lo ^= (uint32_t)(e / K) | ((uint32_t)(e % K) << 8) | (DS_SHAKE << 16);
+  if (i == RW_SHAKE128 - 1) s.hi ^= 0x80000000u;
+  int cnt = 0;
+#pragma unroll 1
+  while (cnt < 256) {  // wave-uniform
+    s = kf_coop(s, c);
+    if (i >= 0 && i < RW_SHAKE128) {
+      pbuf[2 * i] = s.lo;
+      pbuf[2 * i + 1] = s.hi;
+    }
+    wave_phase();
+    uint32_t d1 = Q, d2 = Q;
+    if (lane < 56) {
+      const int b = 3 * lane;
+      const uint32_t v = __builtin_amdgcn_alignbit(pbuf[(b >> 2) + 1], pbuf[b >> 2], 8 * (b & 3));
+      d1 = v & 0xFFF;
+      d2 = (v >> 12) & 0xFFF;
+    }
+    const bool a1 = d1 < (uint32_t)Q, a2 = d2 < (uint32_t)Q;
+    const uint64_t m1 = __ballot(a1), m2 = __ballot(a2);
+    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0)) +
+                    (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0));
+    const int p1 = cnt + pre, p2 = p1 + (a1 ? 1 : 0);
+    if (a1 && p1 < 256) xs16[(((p1 >> 3) * 16 + e) << 3) + (p1 & 7)] = (uint16_t)d1;
+    if (a2 && p2 < 256) xs16[(((p2 >> 3) * 16 + e) << 3) + (p2 & 7)] = (uint16_t)d2;
+    cnt += __popcll(m1) + __popcll(m2);
+    wave_phase();  // this block's parse reads are done before the next block's pbuf writes
+  }
+}
+
+// PRF instance N on one wave: SHAKE256(seed || N) -> 64 eta bytes; word w at ps[w 16 + N].
+template <int ETA>
+__device__ __forceinline__ void prf_coop(const uint64_t* __restrict__ seed, int N, uint64_t* __restrict__ ps,
+                                         const Coop& c) {
+  const int i = c.idx;
+  CState s;
+  if (i >= 0 && i < 4) cs_xor(s, seed[i]);
+  if (i == 4) s.lo ^= (uint32_t)N | (DS_SHAKE << 8);
+  if (i == RW_SHAKE256 - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+  if (ETA == 2) {
+    if (i >= 0 && i < 16) ps[i * 16 + N] = cs_word(s);
+  } else {
+    if (i >= 0 && i < 17) ps[i * 16 + N] = cs_word(s);
+    s = kf_coop(s, c);
+    if (i >= 0 && i < 7) ps[(17 + i) * 16 + N] = cs_word(s);
+  }
+}
+
+struct OneLds {
+  uint4 xs[32 * 16];                // SampleNTT entries (K^2 <= 16)
+  uint64_t ps[PRF_W * 16];          // PRF outputs (2K + 1 <= 9)
+  uint32_t pbuf[ONE_WAVES][44];     // per-wave SampleNTT parse buffers
+  uint64_t seed[4], mp[4], kp[4], kb[4];
   GroupLds g;
 };
 
+// Zero the workgroup's LDS copy of the key material before it exits (LDS is not cleared between
+// workgroups); every thread of the workgroup calls it.
+__device__ __forceinline__ void wipe_one(OneLds& sl) {
+  __syncthreads();
+  uint4* w = (uint4*)&sl;
+  for (int x = threadIdx.x; x < (int)(sizeof(OneLds) / 16); x += 64 * ONE_WAVES) w[x] = make_uint4(0, 0, 0, 0);
+}
+
 template <int K>
-__global__ __launch_bounds__(256) void k_encaps_small(size_t n, const uint8_t* __restrict__ pk,
-                                                      const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
-                                                      uint8_t* __restrict__ ss, int32_t* __restrict__ status,
-                                                      uint64_t* __restrict__ seeds) {
-  __shared__ __attribute__((aligned(16))) SmallLds sl;
+__device__ __forceinline__ void prfs_one(OneLds& sl, int wave, int nprf, int eta1_upto, const Coop& c) {
+#pragma unroll 1
+  for (int N = wave; N < nprf; N += ONE_WAVES) {
+    if (N < eta1_upto)
+      prf_coop<P<K>::ETA1>(sl.seed, N, sl.ps, c);
+    else
+      prf_coop<P<K>::ETA2>(sl.seed, N, sl.ps, c);
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const uint8_t* __restrict__ pk,
+                                                                const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
+                                                                uint8_t* __restrict__ ss, int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave == 0) {
-    if (lane == 0) front_encaps_hs<K>(pk, coins, hs, ss, seeds);  // H(ek), G: the critical chain
-    wave_phase();
-    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2, 16>(seeds + hs * 4, lane, (size_t)lane, K, sl.ps);
-  } else if (wave == 1 && lane < K * K) {
-    xof_entry<K, true, 16>((const uint64_t*)(pk + hs * P<K>::PK + 384 * K), lane, (size_t)lane, sl.xs,
-                           (char*)sl.ring, (uint32_t)lane * 4);
+  const int wave = threadIdx.x >> 6;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
+  SS_MARK(threadIdx.x == 0, 0);
+  if (wave == 0) {  // (K, r) = G(m || H(ek)): the critical chain
+    CState s;
+    coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ek[w]; });
+    const uint64_t h = cs_get(s, (i >= 4 && i < 8) ? i - 4 : 0);
+    const uint64_t* m = (const uint64_t*)(coins + hs * 32);
+    CState g;
+    if (i >= 0 && i < 4) cs_xor(g, m[i]);
+    if (i >= 4 && i < 8) cs_xor(g, h);
+    if (i == 8) {
+      g.lo ^= DS_SHA3;
+      g.hi ^= 0x80000000u;
+    }
+    g = kf_coop(g, c);
+    if (i >= 0 && i < 4) ((uint64_t*)(ss + hs * 32))[i] = cs_word(g);
+    if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
+    SS_MARK(threadIdx.x == 0, 1);
+  } else {
+#pragma unroll 1
+    for (int e = wave - 1; e < K * K; e += ONE_WAVES - 1)
+      xof_coop<K>(ek + 48 * K, e, (uint16_t*)sl.xs, sl.pbuf[wave], c);
+    SS_MARK(threadIdx.x == 64, 3);
   }
   __syncthreads();
+  prfs_one<K>(sl, wave, 2 * K + 1, K, c);
+  SS_MARK(threadIdx.x == 0, 2);
+  __syncthreads();
+  SS_MARK(threadIdx.x == 0, 4);
   if (threadIdx.x < 16)
     encrypt_core_hs<K, 0, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
                               nullptr, nullptr, nullptr, hs, (int)threadIdx.x, sl.g);
+  wipe_one(sl);
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void k_decaps_small(size_t n, const uint8_t* __restrict__ ct,
-                                                      const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss,
-                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ mprime,
-                                                      uint64_t* __restrict__ kprime, uint64_t* __restrict__ kbar) {
-  __shared__ __attribute__((aligned(16))) SmallLds sl;
+__global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const uint8_t* __restrict__ ct,
+                                                                const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss) {
+  __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave == 0) {  // m' = Decrypt, (K', r') = G(m' || h), PRF(r')
-    if (lane < 16) decrypt_core_hs<K>(n, ct, sk, mprime, hs, lane, sl.g);
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const uint8_t* dk = sk + hs * P<K>::SK;
+  SS_MARK(threadIdx.x == 0, 0);
+  if (wave == 0) {  // m' = Decrypt(c), (K', r') = G(m' || h)
+    if (lane < 16) decrypt_core_hs<K, 16>(n, ct, sk, sl.mp, hs, lane, sl.g);
+    SS_MARK(lane == 0, 8);
     wave_phase();
-    if (lane == 0) g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
-    wave_phase();
-    if (lane < 2 * K + 1) prf_inst<P<K>::ETA1, P<K>::ETA2, 16>(seeds + hs * 4, lane, (size_t)lane, K, sl.ps);
+    const uint64_t* h = (const uint64_t*)(dk + 768 * K + 32);
+    CState g;
+    if (i >= 0 && i < 4) cs_xor(g, sl.mp[i]);
+    if (i >= 4 && i < 8) cs_xor(g, h[i - 4]);
+    if (i == 8) {
+      g.lo ^= DS_SHA3;
+      g.hi ^= 0x80000000u;
+    }
+    g = kf_coop(g, c);
+    if (i >= 0 && i < 4) sl.kp[i] = cs_word(g);
+    if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
+    SS_MARK(lane == 0, 9);
   } else if (wave == 1) {  // Kbar = J(z || c) beside it
-    if (lane == 0) j_decaps_hs<K>(ct, sk, hs, kbar);
-  } else if (wave == 2 && lane < K * K) {
-    xof_entry<K, true, 16>((const uint64_t*)(sk + hs * P<K>::SK + 768 * K), lane, (size_t)lane, sl.xs,
-                           (char*)sl.ring, (uint32_t)lane * 4);
+    const uint64_t* z = (const uint64_t*)(dk + 768 * K + 64);
+    const uint64_t* cw = (const uint64_t*)(ct + hs * P<K>::CT);
+    CState s;
+    coop_absorb<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, c, [&](int w) { return w < 4 ? z[w] : cw[w - 4]; });
+    if (i >= 0 && i < 4) sl.kb[i] = cs_word(s);
+    SS_MARK(lane == 0, 11);
+  } else {
+#pragma unroll 1
+    for (int e = wave - 2; e < K * K; e += ONE_WAVES - 2)
+      xof_coop<K>((const uint64_t*)(dk + 768 * K), e, (uint16_t*)sl.xs, sl.pbuf[wave], c);
+    SS_MARK(lane == 0 && wave == 2, 12);
   }
   __syncthreads();
+  prfs_one<K>(sl, wave, 2 * K + 1, K, c);
+  SS_MARK(threadIdx.x == 0, 10);
+  __syncthreads();
+  SS_MARK(threadIdx.x == 0, 4);
   if (threadIdx.x < 16)
     encrypt_core_hs<K, 1, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, sk + 384 * K, (size_t)P<K>::SK,
-                              (const uint8_t*)mprime, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, kprime,
-                              kbar, ss, hs, (int)threadIdx.x, sl.g);
+                              (const uint8_t*)sl.mp, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, sl.kp,
+                              sl.kb, ss, hs, (int)threadIdx.x, sl.g);
+  wipe_one(sl);
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void k_keygen_small(size_t n, const uint8_t* __restrict__ coins,
-                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
-                                                      uint64_t* __restrict__ seeds) {
-  __shared__ __attribute__((aligned(16))) SmallLds sl;
+__global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const uint8_t* __restrict__ coins,
+                                                                uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
+  __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) front_keygen_hs<K>(coins, hs, pk, sk, seeds);  // (rho, sigma) = G(d || k)
-  __syncthreads();
-  if (wave == 0 && lane < 2 * K) {
-    prf_inst<P<K>::ETA1, P<K>::ETA1, 16>(seeds + hs * 4, lane, (size_t)lane, 2 * K, sl.ps);
-  } else if (wave == 1 && lane < K * K) {
-    xof_entry<K, true, 16>((const uint64_t*)(pk + hs * P<K>::PK + 384 * K), lane, (size_t)lane, sl.xs,
-                           (char*)sl.ring, (uint32_t)lane * 4);
+  const int wave = threadIdx.x >> 6;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  uint8_t* ek = pk + hs * P<K>::PK;
+  uint8_t* dk = sk + hs * P<K>::SK;
+  SS_MARK(threadIdx.x == 0, 0);
+  if (wave == 0) {  // (rho, sigma) = G(d || k)
+    const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+    CState g;
+    if (i >= 0 && i < 4) cs_xor(g, d[i]);
+    if (i == 4) g.lo ^= (uint32_t)K | (DS_SHA3 << 8);
+    if (i == RW_SHA3_512 - 1) g.hi ^= 0x80000000u;
+    g = kf_coop(g, c);
+    if (i >= 0 && i < 4) {
+      ((uint64_t*)(ek + 384 * K))[i] = cs_word(g);
+      ((uint64_t*)(dk + 768 * K))[i] = cs_word(g);
+      sl.kp[i] = cs_word(g);  // rho for SampleNTT
+    }
+    if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
+    SS_MARK(threadIdx.x == 0, 13);
   }
   __syncthreads();
-  if (threadIdx.x < 16) keygen_core_hs<K, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, sk, hs, (int)threadIdx.x, sl.g);
+#pragma unroll 1
+  for (int it = wave; it < 2 * K + K * K; it += ONE_WAVES) {  // the 2K PRFs first, then SampleNTT
+    if (it < 2 * K)
+      prf_coop<P<K>::ETA1>(sl.seed, it, sl.ps, c);
+    else
+      xof_coop<K>(sl.kp, it - 2 * K, (uint16_t*)sl.xs, sl.pbuf[wave], c);
+  }
+  SS_MARK(threadIdx.x == 0, 14);
   __syncthreads();
-  if (threadIdx.x == 0) back_keygen_hs<K>(coins, hs, pk, sk);  // H(ek) of the finished ek
+  SS_MARK(threadIdx.x == 0, 4);
+  if (threadIdx.x < 16) keygen_core_hs<K, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, sk, hs, (int)threadIdx.x, sl.g);
+  SS_MARK(threadIdx.x == 0, 16);
+  __syncthreads();
+  if (wave == 0) {  // dk tail: H(ek) || z
+    const uint64_t* ekw = (const uint64_t*)ek;
+    CState s;
+    coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ekw[w]; });
+    uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
+    const uint64_t* z = (const uint64_t*)(coins + hs * 64 + 32);
+    if (i >= 0 && i < 4) {
+      tail[i] = cs_word(s);
+      tail[4 + i] = z[i];
+    }
+    SS_MARK(threadIdx.x == 0, 17);
+  }
+  wipe_one(sl);
 }
 
 // ============================================================ host launchers
@@ -1488,8 +1716,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_keygen_small", s.main, k_keygen_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, coins, pk, sk,
-               v.seeds);
+    QRK_LAUNCH("k_keygen_one", s.main, k_keygen_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, coins,
+               pk, sk);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1512,8 +1740,8 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_encaps_small", s.main, k_encaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, pk, coins, ct,
-               ss, status, v.seeds);
+    QRK_LAUNCH("k_encaps_one", s.main, k_encaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, pk,
+               coins, ct, ss, status);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1536,8 +1764,8 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_decaps_small", s.main, k_decaps_small<K>, dim3((unsigned)n), dim3(256), 0, s.main, n, ct, sk, ss,
-               v.seeds, v.mprime, v.kprime, v.kbar);
+    QRK_LAUNCH("k_decaps_one", s.main, k_decaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, ct, sk,
+               ss);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1562,8 +1790,11 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
   return mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8;
 }
 
+size_t mlkem_small_max() { return QRK_SMALL_MAX; }
+
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
-  if (n == 0) return hipSuccess;
+  // the one-launch kernels (n <= QRK_SMALL_MAX) keep their key material in LDS and wipe it
+  if (n == 0 || n <= QRK_SMALL_MAX) return hipSuccess;
   const size_t C = mlkem::round64(n);
   const mlkem::ScratchView v = mlkem::carve(scratch, a.k, C);
   return hipMemsetAsync(v.seeds, 0, 16 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar
@@ -1603,3 +1834,9 @@ hipError_t mlkem_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* 
 }
 
 }  // namespace qrk
+
+#if QRK_SS_TRACE
+extern "C" int qrk_dbg_ss_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(qrk::mlkem::g_ss_trace), sizeof(qrk::mlkem::g_ss_trace)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -55,6 +55,8 @@ size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 // (ML-KEM: seeds, m', K', Kbar; FrodoKEM: seedSE || k || pkh || mu', the hashed key; HQC: the
 // K-hash message m || u || v and m'), stream-ordered: called after every chunk.
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
+// ML-KEM batches up to this size run as one launch per operation with no scratch key material
+size_t mlkem_small_max();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Phase times inside the ML-KEM single-shot kernels (n = 1), from a -DQRK_SS_TRACE=1 build:
+    tools/build_variant.sh sstrace -DQRK_SS_TRACE=1
+    QRKEM_LIBRARY=quantum-resistant-p2p_amd/qrkem/variants/libqrkem_sstrace.so python3 tools/single_shot_trace.py
+Each phase is microseconds after the kernel's first stamp (100 MHz wall clock), median of N calls."""
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "quantum-resistant-p2p_amd"))
+import torch  # noqa: E402
+from qrkem._native import LIB  # noqa: E402
+from qrkem.batch import BatchKEM  # noqa: E402
+
+ALG, N = sys.argv[1] if len(sys.argv) > 1 else "ML-KEM-768", 100
+fn = LIB.qrk_dbg_ss_trace
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+MARKS = {
+    "keypair": {13: "G(d||k) done", 14: "wave 0 PRF + SampleNTT done", 4: "sync", 16: "core done", 17: "H(ek) done"},
+    "encaps": {1: "H(ek)+G done", 3: "wave 1 SampleNTT done", 2: "PRF done", 4: "sync", 5: "NTT(y) done",
+               6: "u rows done", 7: "v + end"},
+    "decaps": {8: "decrypt done", 9: "G done", 11: "J done", 12: "wave 2 SampleNTT done", 10: "PRF done", 4: "sync",
+               5: "NTT(y) done", 6: "u rows done", 7: "v + select end"},
+}
+
+
+def read():
+    buf = (ctypes.c_ulonglong * 32)()
+    assert fn(buf) == 0
+    return list(buf)
+
+
+eng = BatchKEM(ALG, device=0)
+pk, sk = eng.keypair(n=1)
+ct, ss = eng.encaps(pk)
+torch.cuda.synchronize()
+out = {}
+for op in ("keypair", "encaps", "decaps"):
+    acc = {k: [] for k in MARKS[op]}
+    for _ in range(N):
+        if op == "keypair":
+            eng.keypair(n=1)
+        elif op == "encaps":
+            eng.encaps(pk)
+        else:
+            eng.decaps(sk, ct)
+        torch.cuda.synchronize()
+        t = read()
+        for k in MARKS[op]:
+            acc[k].append((t[k] - t[0]) / 100.0)
+    out[op] = {f"{k}:{v}": round(statistics.median(acc[k]), 2) for k, v in MARKS[op].items()}
+print(json.dumps({"alg": ALG, "phase_us_from_kernel_start": out}))
