@@ -1112,7 +1112,14 @@ __device__ unsigned long long g_ss_trace[32];
   do {                                                        \
     if (cond) g_ss_trace[i] = wall_clock64();                 \
   } while (0)
+#define SS_CLK(cond, i)                                       \
+  do {                                                        \
+    if (cond) g_ss_trace[i] = clock64();                      \
+  } while (0)
 #else
+#define SS_CLK(cond, i) \
+  do {                  \
+  } while (0)
 #define SS_MARK(cond, i) \
   do {                   \
   } while (0)
@@ -1389,7 +1396,7 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
 #ifndef QRK_SMALL_MAX
 #define QRK_SMALL_MAX 256
 #endif
-constexpr int ONE_WAVES = 8;
+constexpr int ONE_WAVES = 12;  // 3 waves per SIMD: the 16-lane cores fit in 170 VGPRs
 
 // ordering between lanes of one wave across phases: a workgroup-scope release / acquire around
 // a wave barrier
@@ -1413,8 +1420,17 @@ __device__ __forceinline__ uint64_t cs_get(const CState& s, int w) {
   const int a = 4 * coop_lane_of(w);
   return ((uint64_t)bperm(a, s.hi) << 32) | bperm(a, s.lo);
 }
-// the permutation as a call (one copy of the unrolled rounds per kernel, not one per call site)
-__device__ __noinline__ CState kf_coop(CState s, Coop c) {
+// the permutation as a call (one copy of the unrolled rounds per kernel, not one per call site);
+// QRK_COOP_CALL=0 inlines it at every call site
+#ifndef QRK_COOP_CALL
+#define QRK_COOP_CALL 1
+#endif
+#if QRK_COOP_CALL
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+CState kf_coop(CState s, Coop c) {
   keccak_f_coop(s.lo, s.hi, c);
   return s;
 }
@@ -1501,11 +1517,15 @@ __device__ __forceinline__ void prf_coop(const uint64_t* __restrict__ seed, int 
 }
 
 struct OneLds {
-  uint4 xs[32 * 16];                // SampleNTT entries (K^2 <= 16)
-  uint64_t ps[PRF_W * 16];          // PRF outputs (2K + 1 <= 9)
-  uint32_t pbuf[ONE_WAVES][44];     // per-wave SampleNTT parse buffers
+  uint4 xs[32 * 16];             // SampleNTT entries (K^2 <= 16)
+  uint64_t ps[PRF_W * 16];       // PRF outputs (2K + 1 <= 9)
+  uint32_t bop[4][16][16];       // NTT(y_j) / NTT(s_j) as basemul operands: word w of lane L at [j][w][L]
+  float ef[4][16][16];           // KeyGen: NTT(e_i), coefficient t of lane L at [i][t][L]
+  uint32_t pbuf[ONE_WAVES][44];  // per-wave SampleNTT parse buffers
   uint64_t seed[4], mp[4], kp[4], kb[4];
-  GroupLds g;
+  uint32_t diff[8];              // Decaps compare: per worker group
+  int flag_seed, flag_kb, n_ready, n_xof, n_done;
+  GroupLds g[8];                 // 16-lane groups: PRF instance N's NTT uses g[N]; rows g[0..K-1], v g[4], Decrypt g[5]
 };
 
 // Zero the workgroup's LDS copy of the key material before it exits (LDS is not cleared between
@@ -1516,15 +1536,128 @@ __device__ __forceinline__ void wipe_one(OneLds& sl) {
   for (int x = threadIdx.x; x < (int)(sizeof(OneLds) / 16); x += 64 * ONE_WAVES) w[x] = make_uint4(0, 0, 0, 0);
 }
 
-template <int K>
-__device__ __forceinline__ void prfs_one(OneLds& sl, int wave, int nprf, int eta1_upto, const Coop& c) {
-#pragma unroll 1
-  for (int N = wave; N < nprf; N += ONE_WAVES) {
-    if (N < eta1_upto)
-      prf_coop<P<K>::ETA1>(sl.seed, N, sl.ps, c);
-    else
-      prf_coop<P<K>::ETA2>(sl.seed, N, sl.ps, c);
+// Cross-wave flags (Decaps, where the J chain must not hold a workgroup barrier): a wave's LDS
+// writes are released before it bumps a counter; readers spin with an acquiring load.
+__device__ __forceinline__ void one_signal(int* p) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void one_wait(int* p, int target) {
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void bop_store(OneLds& sl, int j, const BOp& b, int L) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    sl.bop[j][u][L] = b.b0[u];
+    sl.bop[j][8 + u][L] = b.b1[u];
   }
+}
+__device__ __forceinline__ BOp bop_load(const OneLds& sl, int j, int L) {
+  BOp b;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    b.b0[u] = sl.bop[j][u][L];
+    b.b1[u] = sl.bop[j][8 + u][L];
+  }
+  return b;
+}
+
+// PRF instance N (one wave), then for the secret vector (N < nvec) its NTT on lanes 0-15 into
+// the shared basemul operands (KeyGen also writes NTT(s_j) to dk; KG: NTT(e_i) kept as fp32).
+template <int K, bool KG>
+__device__ __forceinline__ void prf_ntt_one(OneLds& sl, int N, uint8_t* __restrict__ dk, const Coop& c) {
+  constexpr int ETA_V = P<K>::ETA1, ETA_E = KG ? P<K>::ETA1 : P<K>::ETA2;
+  if (N < K)
+    prf_coop<ETA_V>(sl.seed, N, sl.ps, c);
+  else
+    prf_coop<ETA_E>(sl.seed, N, sl.ps, c);
+  const int L = threadIdx.x & 63;
+  if (L < 16 && (N < K || KG)) {
+    wave_phase();
+    PF16 f;
+    cbd_f<ETA_V>(f, cbd_load<ETA_V, 16>(sl.ps, (size_t)N, L));
+    GroupLds& g = sl.g[N];  // N < 2K <= 8 (KeyGen), N < K otherwise
+    contig_to_stride_f(f, (float*)g.poly, L);
+    ntt_fwd_f<false>(f, (float*)g.poly, L);
+    if (N < K) {
+      bop_store(sl, N, make_bop_f(f, L), L);
+      if (KG) {
+        P16 t;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
+        encode12(t, dk + 384 * N, L);
+      }
+    } else {
+#pragma unroll
+      for (int x = 0; x < 16; ++x) sl.ef[N - K][x][L] = f.v[x];
+    }
+  }
+}
+
+// u_i = Compress_du(NTT^-1(sum_j A[i][j]^T o y_j) + e1_i) on one 16-lane group: written to c (MODE
+// 0) or compared with it into diff (MODE 1).
+template <int K, int MODE>
+__device__ __forceinline__ void enc_row_one(const OneLds& sl, int i, uint8_t* __restrict__ c, uint32_t& diff,
+                                            GroupLds& g, int L) {
+  constexpr int DU = P<K>::DU;
+  int acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<16>(sl.xs, (size_t)(i * K + j), L), bop_load(sl, j, L));
+  const CbdRaw er = cbd_load<P<K>::ETA2, 16>(sl.ps, (size_t)(K + i), L);
+  CmpWords<DU> cw;
+  if (MODE) cw = cmp_load<DU>(c + 32 * DU * i, L);
+  PF16 uf;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) uf.v[t] = acc_to_f(acc[t]);
+  ntt_inv_f(uf, (float*)g.poly, L);
+  stride_to_contig_f(uf, (float*)g.poly, L);
+  PF16 ef;
+  cbd_f<P<K>::ETA2>(ef, er);
+  P16 u;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon_f(uf.v[t] + ef.v[t]));
+  pack_bits<DU>(u, g, L);
+  if (MODE)
+    flush_cmp<DU>(g, cw, diff, L);
+  else
+    flush_bits<DU>(g, c + 32 * DU * i, nullptr, diff, true, L);
+}
+
+// v = Compress_dv(NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)) on one 16-lane group; returns
+// the FIPS 203 modulus-check failure of ek (Encaps status).
+template <int K, int MODE>
+__device__ __forceinline__ bool enc_v_one(const OneLds& sl, const uint8_t* __restrict__ ek, const uint8_t* __restrict__ m,
+                                          uint8_t* __restrict__ c, uint32_t& diff, GroupLds& g, int L) {
+  constexpr int DU = P<K>::DU, DV = P<K>::DV;
+  int acc[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) acc[t] = 0;
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < K; ++j) basemul_acc(acc, decode12(ek + 384 * j, bad, L), bop_load(sl, j, L));
+  const CbdRaw er = cbd_load<P<K>::ETA2, 16>(sl.ps, (size_t)(2 * K), L);
+  const uint32_t mb = (uint32_t)m[2 * L] | ((uint32_t)m[2 * L + 1] << 8);
+  PF16 vf;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) vf.v[t] = acc_to_f(acc[t]);
+  ntt_inv_f(vf, (float*)g.poly, L);
+  stride_to_contig_f(vf, (float*)g.poly, L);
+  PF16 ef;
+  cbd_f<P<K>::ETA2>(ef, er);
+  P16 v;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const float mu = ((mb >> t) & 1) ? (float)((Q + 1) / 2) : 0.0f;
+    v.v[t] = compress<DV>(canon_f(vf.v[t] + ef.v[t] + mu));
+  }
+  pack_bits<DV>(v, g, L);
+  flush_bits<DV>(g, c + 32 * DU * K, MODE ? c + 32 * DU * K : nullptr, diff, true, L);
+  return group_or(bad ? 1u : 0u) != 0;
 }
 
 template <int K>
@@ -1533,12 +1666,14 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
                                                                 uint8_t* __restrict__ ss, int32_t* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const Coop c = coop_init();
   const int i = c.idx;
   const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
   SS_MARK(threadIdx.x == 0, 0);
+  SS_CLK(threadIdx.x == 0, 20);
   if (wave == 0) {  // (K, r) = G(m || H(ek)): the critical chain
+    __builtin_amdgcn_s_setprio(3);
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ek[w]; });
     const uint64_t h = cs_get(s, (i >= 4 && i < 8) ? i - 4 : 0);
@@ -1553,7 +1688,9 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
     g = kf_coop(g, c);
     if (i >= 0 && i < 4) ((uint64_t*)(ss + hs * 32))[i] = cs_word(g);
     if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
+    __builtin_amdgcn_s_setprio(0);
     SS_MARK(threadIdx.x == 0, 1);
+    SS_CLK(threadIdx.x == 0, 21);
   } else {
 #pragma unroll 1
     for (int e = wave - 1; e < K * K; e += ONE_WAVES - 1)
@@ -1561,13 +1698,19 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
     SS_MARK(threadIdx.x == 64, 3);
   }
   __syncthreads();
-  prfs_one<K>(sl, wave, 2 * K + 1, K, c);
+  if (wave < 2 * K + 1) prf_ntt_one<K, false>(sl, wave, nullptr, c);  // PRF(r, N), NTT(y_N)
   SS_MARK(threadIdx.x == 0, 2);
   __syncthreads();
   SS_MARK(threadIdx.x == 0, 4);
-  if (threadIdx.x < 16)
-    encrypt_core_hs<K, 0, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
-                              nullptr, nullptr, nullptr, hs, (int)threadIdx.x, sl.g);
+  uint8_t* cc = ct + hs * P<K>::CT;
+  uint32_t diff = 0;
+  if (wave == 0 && (lane >> 4) < K) {
+    enc_row_one<K, 0>(sl, lane >> 4, cc, diff, sl.g[lane >> 4], lane & 15);
+  } else if (wave == 1 && lane < 16) {
+    const bool bad = enc_v_one<K, 0>(sl, (const uint8_t*)ek, coins + hs * 32, cc, diff, sl.g[4], lane);
+    if (status && lane == 0) status[hs] = bad ? -1 : 0;
+  }
+  SS_MARK(threadIdx.x == 0, 7);
   wipe_one(sl);
 }
 
@@ -1580,9 +1723,13 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
   const Coop c = coop_init();
   const int i = c.idx;
   const uint8_t* dk = sk + hs * P<K>::SK;
+  uint8_t* cc = const_cast<uint8_t*>(ct) + hs * P<K>::CT;
+  constexpr int XW = ONE_WAVES - 3;  // SampleNTT waves 2 .. ONE_WAVES - 2; the last wave computes v
+  if (threadIdx.x == 0) sl.flag_seed = sl.flag_kb = sl.n_ready = sl.n_xof = sl.n_done = 0;
+  __syncthreads();
   SS_MARK(threadIdx.x == 0, 0);
-  if (wave == 0) {  // m' = Decrypt(c), (K', r') = G(m' || h)
-    if (lane < 16) decrypt_core_hs<K, 16>(n, ct, sk, sl.mp, hs, lane, sl.g);
+  if (wave == 0) {  // m' = Decrypt(c), (K', r') = G(m' || h), PRF(r', 0), then the u rows and the select
+    if (lane < 16) decrypt_core_hs<K, 16>(n, ct, sk, sl.mp, hs, lane, sl.g[5]);
     SS_MARK(lane == 0, 8);
     wave_phase();
     const uint64_t* h = (const uint64_t*)(dk + 768 * K + 32);
@@ -1596,29 +1743,63 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
     g = kf_coop(g, c);
     if (i >= 0 && i < 4) sl.kp[i] = cs_word(g);
     if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
+    one_signal(&sl.flag_seed);
     SS_MARK(lane == 0, 9);
-  } else if (wave == 1) {  // Kbar = J(z || c) beside it
+    prf_ntt_one<K, false>(sl, 0, nullptr, c);
+    one_signal(&sl.n_ready);
+    one_wait(&sl.n_ready, 2 * K + 1);
+    one_wait(&sl.n_xof, K * K);
+    SS_MARK(lane == 0, 4);
+    uint32_t diff = 0;
+    if ((lane >> 4) < K) enc_row_one<K, 1>(sl, lane >> 4, cc, diff, sl.g[lane >> 4], lane & 15);
+    diff = group_or(diff);
+    if ((lane & 15) == 0 && (lane >> 4) < K) sl.diff[lane >> 4] = diff;
+    one_wait(&sl.n_done, 1);   // v
+    one_wait(&sl.flag_kb, 1);  // Kbar
+    SS_MARK(lane == 0, 6);
+    if (lane < 8) {  // constant-time select: ss = (c == c') ? K' : Kbar
+      uint32_t d = sl.diff[4];
+#pragma unroll
+      for (int r = 0; r < K; ++r) d |= sl.diff[r];
+      const uint32_t mask = (uint32_t)(((uint64_t)d - 1u) >> 32);  // all-ones iff d == 0, no branch
+      const uint32_t kp = ((const uint32_t*)sl.kp)[lane], kb = ((const uint32_t*)sl.kb)[lane];
+      ((uint32_t*)(ss + hs * 32))[lane] = (kp & mask) | (kb & ~mask);
+    }
+    SS_MARK(lane == 0, 7);
+  } else if (wave == 1) {  // Kbar = J(z || c) beside everything else
+    __builtin_amdgcn_s_setprio(3);
     const uint64_t* z = (const uint64_t*)(dk + 768 * K + 64);
-    const uint64_t* cw = (const uint64_t*)(ct + hs * P<K>::CT);
+    const uint64_t* cw = (const uint64_t*)cc;
     CState s;
     coop_absorb<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, c, [&](int w) { return w < 4 ? z[w] : cw[w - 4]; });
     if (i >= 0 && i < 4) sl.kb[i] = cs_word(s);
+    __builtin_amdgcn_s_setprio(0);
+    one_signal(&sl.flag_kb);
     SS_MARK(lane == 0, 11);
-  } else {
+  } else if (wave < ONE_WAVES - 1) {  // SampleNTT, then PRF(r', N) for N = wave - 1
 #pragma unroll 1
-    for (int e = wave - 2; e < K * K; e += ONE_WAVES - 2)
+    for (int e = wave - 2; e < K * K; e += XW) {
       xof_coop<K>((const uint64_t*)(dk + 768 * K), e, (uint16_t*)sl.xs, sl.pbuf[wave], c);
+      one_signal(&sl.n_xof);
+    }
     SS_MARK(lane == 0 && wave == 2, 12);
+    const int N = wave - 1;
+    if (N < 2 * K + 1) {
+      one_wait(&sl.flag_seed, 1);
+      prf_ntt_one<K, false>(sl, N, nullptr, c);
+      one_signal(&sl.n_ready);
+    }
+    SS_MARK(lane == 0 && wave == 2, 10);
+  } else {  // v
+    one_wait(&sl.n_ready, 2 * K + 1);
+    if (lane < 16) {
+      uint32_t diff = 0;
+      enc_v_one<K, 1>(sl, dk + 384 * K, (const uint8_t*)sl.mp, cc, diff, sl.g[4], lane);
+      diff = group_or(diff);
+      if (lane == 0) sl.diff[4] = diff;
+    }
+    one_signal(&sl.n_done);
   }
-  __syncthreads();
-  prfs_one<K>(sl, wave, 2 * K + 1, K, c);
-  SS_MARK(threadIdx.x == 0, 10);
-  __syncthreads();
-  SS_MARK(threadIdx.x == 0, 4);
-  if (threadIdx.x < 16)
-    encrypt_core_hs<K, 1, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, sk + 384 * K, (size_t)P<K>::SK,
-                              (const uint8_t*)sl.mp, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, sl.kp,
-                              sl.kb, ss, hs, (int)threadIdx.x, sl.g);
   wipe_one(sl);
 }
 
@@ -1627,7 +1808,7 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
                                                                 uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const Coop c = coop_init();
   const int i = c.idx;
   uint8_t* ek = pk + hs * P<K>::PK;
@@ -1650,16 +1831,28 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
   }
   __syncthreads();
 #pragma unroll 1
-  for (int it = wave; it < 2 * K + K * K; it += ONE_WAVES) {  // the 2K PRFs first, then SampleNTT
+  for (int it = wave; it < 2 * K + K * K; it += ONE_WAVES) {  // the 2K PRFs (+ NTTs) first, then SampleNTT
     if (it < 2 * K)
-      prf_coop<P<K>::ETA1>(sl.seed, it, sl.ps, c);
+      prf_ntt_one<K, true>(sl, it, dk, c);
     else
       xof_coop<K>(sl.kp, it - 2 * K, (uint16_t*)sl.xs, sl.pbuf[wave], c);
   }
   SS_MARK(threadIdx.x == 0, 14);
   __syncthreads();
   SS_MARK(threadIdx.x == 0, 4);
-  if (threadIdx.x < 16) keygen_core_hs<K, 16>(n, 1, (const uint64_t*)sl.xs, sl.ps, pk, sk, hs, (int)threadIdx.x, sl.g);
+  if (wave == 0 && (lane >> 4) < K) {  // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i, one group per row
+    const int r = lane >> 4, L = lane & 15;
+    int acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<16>(sl.xs, (size_t)(j * K + r), L), bop_load(sl, j, L));
+    P16 t;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) t.v[x] = canon_f(acc_to_f(acc[x]) + sl.ef[r][x][L]);
+    encode12(t, ek + 384 * r, L);
+    encode12(t, dk + 384 * K + 384 * r, L);
+  }
   SS_MARK(threadIdx.x == 0, 16);
   __syncthreads();
   if (wave == 0) {  // dk tail: H(ek) || z

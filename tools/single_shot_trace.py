@@ -18,11 +18,10 @@ ALG, N = sys.argv[1] if len(sys.argv) > 1 else "ML-KEM-768", 100
 fn = LIB.qrk_dbg_ss_trace
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 MARKS = {
-    "keypair": {13: "G(d||k) done", 14: "wave 0 PRF + SampleNTT done", 4: "sync", 16: "core done", 17: "H(ek) done"},
-    "encaps": {1: "H(ek)+G done", 3: "wave 1 SampleNTT done", 2: "PRF done", 4: "sync", 5: "NTT(y) done",
-               6: "u rows done", 7: "v + end"},
-    "decaps": {8: "decrypt done", 9: "G done", 11: "J done", 12: "wave 2 SampleNTT done", 10: "PRF done", 4: "sync",
-               5: "NTT(y) done", 6: "u rows done", 7: "v + select end"},
+    "keypair": {13: "G(d||k) done", 14: "wave 0 PRF/NTT + SampleNTT done", 4: "sync", 16: "t rows done", 17: "H(ek) done"},
+    "encaps": {1: "H(ek)+G done", 3: "wave 1 SampleNTT done", 2: "wave 0 PRF + NTT(y_0) done", 4: "sync", 7: "u rows done"},
+    "decaps": {8: "decrypt done", 9: "G done", 12: "wave 2 SampleNTT done", 10: "wave 2 PRF done", 4: "rows start",
+               11: "J done", 6: "rows done, v + Kbar ready", 7: "select done"},
 }
 
 
@@ -39,6 +38,7 @@ torch.cuda.synchronize()
 out = {}
 for op in ("keypair", "encaps", "decaps"):
     acc = {k: [] for k in MARKS[op]}
+    mhz = []
     for _ in range(N):
         if op == "keypair":
             eng.keypair(n=1)
@@ -50,5 +50,9 @@ for op in ("keypair", "encaps", "decaps"):
         t = read()
         for k in MARKS[op]:
             acc[k].append((t[k] - t[0]) / 100.0)
+        if op == "encaps":
+            mhz.append((t[21] - t[20]) / ((t[1] - t[0]) / 100.0))
     out[op] = {f"{k}:{v}": round(statistics.median(acc[k]), 2) for k, v in MARKS[op].items()}
+    if op == "encaps":  # shader clock over H(ek) + G: clock64 cycles / wall-clock time
+        out[op]["shader_MHz_during_H_G"] = round(statistics.median(mhz), 1)
 print(json.dumps({"alg": ALG, "phase_us_from_kernel_start": out}))
