@@ -1343,8 +1343,8 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;
-  const uint8_t* c = ct + hs * P<K>::CT;
-  const uint8_t* dk = sk + hs * P<K>::SK;
+  const uint8_t* c = ct + (TW == 64 ? hs : 0) * P<K>::CT;  // the small path passes LDS copies
+  const uint8_t* dk = sk + (TW == 64 ? hs : 0) * P<K>::SK;
   int acc[16];
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = 0;
@@ -1522,6 +1522,7 @@ struct OneLds {
   uint32_t bop[4][16][16];       // NTT(y_j) / NTT(s_j) as basemul operands: word w of lane L at [j][w][L]
   float ef[4][16][16];           // KeyGen: NTT(e_i), coefficient t of lane L at [i][t][L]
   uint32_t pbuf[ONE_WAVES][44];  // per-wave SampleNTT parse buffers
+  uint64_t io[600];              // the handshake's inputs (Encaps ek | m, Decaps c | dk; KeyGen ek)
   uint64_t seed[4], mp[4], kp[4], kb[4];
   uint32_t diff[8];              // Decaps compare: per worker group
   int flag_seed, flag_kb, n_ready, n_xof, n_done;
@@ -1529,9 +1530,12 @@ struct OneLds {
 };
 
 // Zero the workgroup's LDS copy of the key material before it exits (LDS is not cleared between
-// workgroups); every thread of the workgroup calls it.
-__device__ __forceinline__ void wipe_one(OneLds& sl) {
+// workgroups); every thread of the workgroup calls it.  With a completion flag (single-shot host
+// calls) the outputs are first made visible at system scope, then the flag is stored.
+__device__ __forceinline__ void wipe_one(OneLds& sl, uint32_t* done, uint32_t ticket) {
+  if (done) __threadfence_system();
   __syncthreads();
+  if (done && threadIdx.x == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   uint4* w = (uint4*)&sl;
   for (int x = threadIdx.x; x < (int)(sizeof(OneLds) / 16); x += 64 * ONE_WAVES) w[x] = make_uint4(0, 0, 0, 0);
 }
@@ -1546,6 +1550,12 @@ __device__ __forceinline__ void one_signal(int* p) {
 __device__ __forceinline__ void one_wait(int* p, int target) {
   while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Copy one handshake's inputs (host-mapped or device memory) into LDS in one parallel burst: the
+// zero-copy single-shot calls then pay one PCIe round trip instead of one per dependent load.
+__device__ __forceinline__ void stage_in(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, int words) {
+  for (int w = threadIdx.x; w < words; w += 64 * ONE_WAVES) dst[w] = src[w];
 }
 
 __device__ __forceinline__ void bop_store(OneLds& sl, int j, const BOp& b, int L) {
@@ -1663,21 +1673,26 @@ __device__ __forceinline__ bool enc_v_one(const OneLds& sl, const uint8_t* __res
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const uint8_t* __restrict__ pk,
                                                                 const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
-                                                                uint8_t* __restrict__ ss, int32_t* __restrict__ status) {
+                                                                uint8_t* __restrict__ ss, int32_t* __restrict__ status,
+                                                                uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const Coop c = coop_init();
   const int i = c.idx;
-  const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
+  constexpr int EKW = P<K>::PK / 8;
   SS_MARK(threadIdx.x == 0, 0);
   SS_CLK(threadIdx.x == 0, 20);
+  stage_in(sl.io, (const uint64_t*)(pk + hs * P<K>::PK), EKW);
+  stage_in(sl.io + EKW, (const uint64_t*)(coins + hs * 32), 4);
+  __syncthreads();
+  const uint64_t* ek = sl.io;
   if (wave == 0) {  // (K, r) = G(m || H(ek)): the critical chain
     __builtin_amdgcn_s_setprio(3);
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ek[w]; });
     const uint64_t h = cs_get(s, (i >= 4 && i < 8) ? i - 4 : 0);
-    const uint64_t* m = (const uint64_t*)(coins + hs * 32);
+    const uint64_t* m = sl.io + EKW;
     CState g;
     if (i >= 0 && i < 4) cs_xor(g, m[i]);
     if (i >= 4 && i < 8) cs_xor(g, h);
@@ -1707,29 +1722,33 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   if (wave == 0 && (lane >> 4) < K) {
     enc_row_one<K, 0>(sl, lane >> 4, cc, diff, sl.g[lane >> 4], lane & 15);
   } else if (wave == 1 && lane < 16) {
-    const bool bad = enc_v_one<K, 0>(sl, (const uint8_t*)ek, coins + hs * 32, cc, diff, sl.g[4], lane);
+    const bool bad = enc_v_one<K, 0>(sl, (const uint8_t*)ek, (const uint8_t*)(sl.io + EKW), cc, diff, sl.g[4], lane);
     if (status && lane == 0) status[hs] = bad ? -1 : 0;
   }
   SS_MARK(threadIdx.x == 0, 7);
-  wipe_one(sl);
+  wipe_one(sl, done, ticket);
 }
 
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const uint8_t* __restrict__ ct,
-                                                                const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss) {
+                                                                const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss,
+                                                                uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const Coop c = coop_init();
   const int i = c.idx;
-  const uint8_t* dk = sk + hs * P<K>::SK;
-  uint8_t* cc = const_cast<uint8_t*>(ct) + hs * P<K>::CT;
+  constexpr int CTW = P<K>::CT / 8, SKW = P<K>::SK / 8;
+  stage_in(sl.io, (const uint64_t*)(ct + hs * P<K>::CT), CTW);
+  stage_in(sl.io + CTW, (const uint64_t*)(sk + hs * P<K>::SK), SKW);
+  uint8_t* cc = (uint8_t*)sl.io;                   // the received ciphertext (LDS copy)
+  const uint8_t* dk = (const uint8_t*)(sl.io + CTW);  // dk (LDS copy)
   constexpr int XW = ONE_WAVES - 3;  // SampleNTT waves 2 .. ONE_WAVES - 2; the last wave computes v
   if (threadIdx.x == 0) sl.flag_seed = sl.flag_kb = sl.n_ready = sl.n_xof = sl.n_done = 0;
   __syncthreads();
   SS_MARK(threadIdx.x == 0, 0);
   if (wave == 0) {  // m' = Decrypt(c), (K', r') = G(m' || h), PRF(r', 0), then the u rows and the select
-    if (lane < 16) decrypt_core_hs<K, 16>(n, ct, sk, sl.mp, hs, lane, sl.g[5]);
+    if (lane < 16) decrypt_core_hs<K, 16>(n, cc, dk, sl.mp, hs, lane, sl.g[5]);
     SS_MARK(lane == 0, 8);
     wave_phase();
     const uint64_t* h = (const uint64_t*)(dk + 768 * K + 32);
@@ -1800,12 +1819,13 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
     }
     one_signal(&sl.n_done);
   }
-  wipe_one(sl);
+  wipe_one(sl, done, ticket);
 }
 
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const uint8_t* __restrict__ coins,
-                                                                uint8_t* __restrict__ pk, uint8_t* __restrict__ sk) {
+                                                                uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                                uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1825,6 +1845,7 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
       ((uint64_t*)(ek + 384 * K))[i] = cs_word(g);
       ((uint64_t*)(dk + 768 * K))[i] = cs_word(g);
       sl.kp[i] = cs_word(g);  // rho for SampleNTT
+      sl.io[48 * K + i] = cs_word(g);  // ek's LDS copy (hashed below)
     }
     if (i >= 4 && i < 8) sl.seed[i - 4] = cs_word(g);
     SS_MARK(threadIdx.x == 0, 13);
@@ -1852,11 +1873,12 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
     for (int x = 0; x < 16; ++x) t.v[x] = canon_f(acc_to_f(acc[x]) + sl.ef[r][x][L]);
     encode12(t, ek + 384 * r, L);
     encode12(t, dk + 384 * K + 384 * r, L);
+    encode12(t, (uint8_t*)sl.io + 384 * r, L);
   }
   SS_MARK(threadIdx.x == 0, 16);
   __syncthreads();
   if (wave == 0) {  // dk tail: H(ek) || z
-    const uint64_t* ekw = (const uint64_t*)ek;
+    const uint64_t* ekw = sl.io;
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ekw[w]; });
     uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
@@ -1867,7 +1889,7 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
     }
     SS_MARK(threadIdx.x == 0, 17);
   }
-  wipe_one(sl);
+  wipe_one(sl, done, ticket);
 }
 
 // ============================================================ host launchers
@@ -1910,7 +1932,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
     QRK_LAUNCH("k_keygen_one", s.main, k_keygen_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, coins,
-               pk, sk);
+               pk, sk, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1934,7 +1956,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
     QRK_LAUNCH("k_encaps_one", s.main, k_encaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, pk,
-               coins, ct, ss, status);
+               coins, ct, ss, status, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
@@ -1958,7 +1980,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
     QRK_LAUNCH("k_decaps_one", s.main, k_decaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, ct, sk,
-               ss);
+               ss, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;

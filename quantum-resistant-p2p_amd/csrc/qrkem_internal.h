@@ -66,6 +66,10 @@ struct Streams {
   hipStream_t main = nullptr;
   hipStream_t aux = nullptr;  // nullptr: single-stream schedule
   hipEvent_t fork = nullptr, join = nullptr;
+  // single-shot completion flag (fine-grained host memory, device address): the one-launch ML-KEM
+  // kernels store `ticket` there once their outputs are visible to the host
+  uint32_t* done = nullptr;
+  uint32_t ticket = 0;
 };
 
 // All pointers are device pointers; n handshakes processed as one chunk

@@ -1,0 +1,8 @@
+set -o pipefail
+mkdir -p gpurun_out/r2u
+g++ -O2 -Iinclude tools/oqs_latency.cpp -Lquantum-resistant-p2p_amd/qrkem -lqrkem -Wl,-rpath,$PWD/quantum-resistant-p2p_amd/qrkem -o /tmp/oqs_latency &&
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_mlkem.py tests/test_gpu_edges.py tests/test_gpu_handshake.py tests/test_gpu_ordering.py tests/test_abi.py > gpurun_out/r2u/t.log 2>&1 &&
+timeout -k 10 60 /tmp/oqs_latency ML-KEM-768 > gpurun_out/r2u/c_api.json &&
+timeout -k 10 60 /tmp/oqs_latency ML-KEM-512 >> gpurun_out/r2u/c_api.json &&
+timeout -k 10 60 /tmp/oqs_latency ML-KEM-1024 >> gpurun_out/r2u/c_api.json &&
+timeout -k 10 200 python3 tools/single_shot_breakdown.py > gpurun_out/r2u/breakdown.json 2> gpurun_out/r2u/ss.err

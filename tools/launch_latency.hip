@@ -58,8 +58,35 @@ int main() {
     c.push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
     (void)hipStreamSynchronize(st);
   }
+  // per-call host cost of the API calls a single-shot ABI call makes around its launch
+  std::vector<double> er, gdc, gd, sd, lfs;
+  for (int i = 0; i < N; ++i) {
+    const unsigned v = (unsigned)i + 100000;
+    auto t0 = clk::now();
+    hipLaunchKernelGGL(k_flag, dim3(1), dim3(64), 0, st, flag, v);
+    auto t1 = clk::now();
+    (void)hipEventRecord(ev, st);
+    auto t2 = clk::now();
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != v) {
+    }
+    auto t3 = clk::now();
+    int cnt = 0, dev = 0;
+    (void)hipGetDeviceCount(&cnt);
+    auto t4 = clk::now();
+    (void)hipGetDevice(&dev);
+    auto t5 = clk::now();
+    (void)hipSetDevice(dev);
+    auto t6 = clk::now();
+    (void)hipStreamSynchronize(st);
+    er.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
+    lfs.push_back(std::chrono::duration<double, std::micro>(t3 - t0).count());
+    gdc.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
+    gd.push_back(std::chrono::duration<double, std::micro>(t5 - t4).count());
+    sd.push_back(std::chrono::duration<double, std::micro>(t6 - t5).count());
+  }
   printf("{\"launch_only_us\": %.1f, \"launch_stream_sync_us\": %.1f, \"launch_event_sync_us\": %.1f, "
-         "\"launch_flag_spin_us\": %.1f}\n",
-         med(d), med(a), med(b), med(c));
+         "\"launch_flag_spin_us\": %.1f, \"event_record_us\": %.2f, \"launch_record_spin_us\": %.1f, "
+         "\"get_device_count_us\": %.2f, \"get_device_us\": %.2f, \"set_device_us\": %.2f}\n",
+         med(d), med(a), med(b), med(c), med(er), med(lfs), med(gdc), med(gd), med(sd));
   return 0;
 }
