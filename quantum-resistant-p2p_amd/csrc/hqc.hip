@@ -70,7 +70,7 @@ template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9,
 template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 384, 384> {};
 
 // ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
-struct GfTabs {
+struct alignas(4) GfTabs {
   uint8_t exp[512];
   uint8_t log[256];
 };
@@ -329,49 +329,118 @@ __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, 
 }
 
 // The spec's duplicate removal (oracle/src/hqc.c fixed_weight): for i = w-2 .. 0, s_i := i when
-// s_i equals some s_j with j > i.  That serial loop has a closed form (tests/test_hqc_dedupe.py
-// checks it against the loop): s_i is replaced iff
-//   s_j == s_i for some j > i   (the original values; every lower copy of a value is replaced), or
-//   i < s_i < w and s_{s_i} is replaced   (s_i collides with the index written at j = s_i).
-// The second term is a chain through strictly increasing indices; pointer jumping resolves it in
-// ceil(log2 w) rounds.  All threads of the workgroup take part, no data-dependent control flow.
-// NV supports of weight WT, vector v at SS + v * WMAX; PJ: NV * WT words of scratch
-// (bit 31 = replaced so far along the chain, low 16 bits = next chain index or NONE).
-template <int L, int NV, int WT>
-__device__ __forceinline__ void dedupe_wg(uint32_t* SS, uint32_t* PJ) {
-  using P = HQ<L>;
+// s_i equals some s_j with j > i (the current, possibly replaced, s_j).
+// Duplicate removal of one vector of weight WT (<= 192) on one wave, element 64e + l in lane l's
+// register v[e], no LDS round trips and no workgroup barriers (other waves work on their own
+// vectors meanwhile).  The spec's loop has a closed form (tests/test_hqc_dedupe.py checks it and
+// this wave restatement against the loop): s_i is replaced iff
+//   s_j == s_i for some j > i   (the original values), or
+//   i < s_i < w and s_{s_i} is replaced   (a chain through strictly increasing indices).
+// The first term: every s_j broadcast once (v_readlane) and compared with all lanes (a ballot per
+// register, masked to j > i, OR-ed into 64-bit lane masks); the chain: pointer jumping over
+// (replaced, next) words gathered with ds_bpermute, ceil(log2 w) rounds.
+template <int WT>
+__device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
+  constexpr int NE = (WT + 63) / 64;
   constexpr uint32_t NONE = 0xFFFFu, REP = 0x80000000u;
-  constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);  // 2^ROUNDS >= WT chain nodes
-  static_assert(WT <= P::WMAX && WT > 1, "weight");
-  for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
-    const int v = e / WT, i = e - v * WT;
-    const uint32_t* s = SS + v * P::WMAX;
-    const uint32_t o = s[i];
-    uint32_t dup = 0;
-#pragma unroll 8
-    for (int j = 0; j < WT; ++j) dup |= (uint32_t)((j > i) & (s[j] == o));
-    const uint32_t ptr = (o > (uint32_t)i && o < (uint32_t)WT) ? o : NONE;
-    PJ[e] = (dup ? REP : 0u) | ptr;
+  constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);
+  static_assert(NE <= 3 && WT > 1, "weight");
+  const int lane = threadIdx.x & 63;
+  uint32_t v[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
+  uint64_t dup[NE] = {};
+#pragma unroll
+  for (int j = 1; j < WT; ++j) {
+    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      if (64 * e >= j) continue;  // no i < j in this register
+      uint64_t m = __ballot(v[e] == sj);
+      if (64 * e + 64 > j) m &= (1ull << (j - 64 * e)) - 1;  // i < j
+      dup[e] |= m;
+    }
   }
-  __syncthreads();
-  // in place: a node read mid-round is either its old or its new (rep, ptr) pair, both of which
-  // keep "rep = OR over the chain from here up to ptr"; jumps still at least double per round
+  uint32_t x[NE];  // REP | next chain index (or NONE)
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const uint32_t i = 64 * e + lane;
+    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
+    x[e] = ((dup[e] >> lane) & 1 ? REP : 0u) | ptr;
+  }
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
-    for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
-      const int v = e / WT, i = e - v * WT;
-      const uint32_t x = PJ[e], p = x & NONE;
-      const uint32_t y = PJ[v * WT + (p == NONE ? i : (int)p)];
-      PJ[e] = (x & REP) | y;
+    uint32_t y[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const uint32_t p = x[e] & NONE;
+      const int src = 4 * (int)(p & 63);  // lane of element p (any lane when p == NONE)
+      uint32_t g = 0;
+#pragma unroll
+      for (int f = 0; f < NE; ++f) {
+        const uint32_t gf = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)x[f]);
+        g = (p >> 6) == (uint32_t)f ? gf : g;
+      }
+      y[e] = p == NONE ? x[e] : ((x[e] & REP) | g);
     }
-    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < NE; ++e) x[e] = y[e];
   }
-  for (int e = threadIdx.x; e < NV * WT; e += P::TPB) {
-    const int v = e / WT, i = e - v * WT;
-    if (PJ[e] & REP) SS[v * P::WMAX + i] = (uint32_t)i;
-  }
-  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < NE; ++e)
+    if (64 * e + lane < WT) s[64 * e + lane] = (x[e] & REP) ? (uint32_t)(64 * e + lane) : v[e];
 }
+
+// The spec's loop itself on one wave: step i (w-2 .. 0) broadcasts s_i (v_readlane), compares it
+// with every current s_j (a ballot per register, masked to j > i) and replaces s_i by i on a hit
+// (a wave-uniform decision): w - 1 dependent steps.
+template <int WT>
+__device__ __forceinline__ void dedupe_wave_loop(uint32_t* s) {
+  constexpr int NE = (WT + 63) / 64;
+  static_assert(NE <= 3 && WT > 1, "weight");
+  const int lane = threadIdx.x & 63;
+  uint32_t v[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
+#pragma unroll
+  for (int i = WT - 2; i >= 0; --i) {
+    const int ei = i >> 6, li = i & 63;
+    const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)v[ei], li);
+    uint64_t hit = 0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      if (64 * e + 63 <= i) continue;  // no j > i in this register
+      uint64_t m = __ballot(v[e] == si);
+      if (64 * e <= i) m &= ~0ull << (i - 64 * e + 1);
+      hit |= m;
+    }
+    if (hit) v[ei] = lane == li ? (uint32_t)i : v[ei];
+  }
+#pragma unroll
+  for (int e = 0; e < NE; ++e)
+    if (64 * e + lane < WT) s[64 * e + lane] = v[e];
+}
+
+// QRK_HQC_DEDUPE_CF: 1 closed form (default), 0 the serial loop.  A/B on one box
+// (profiles/r2/ab_hqc_dedupe_staging.jsonl): HQC-128 / 256 enc+dec 17.26e6 / 3.76e6 (closed form,
+// LDS staging) against 16.37e6 / 3.43e6 with round 1's workgroup-wide dedupe.
+#ifndef QRK_HQC_DEDUPE_CF
+#define QRK_HQC_DEDUPE_CF 1
+#endif
+template <int WT>
+__device__ __forceinline__ void dedupe_wave(uint32_t* s) {
+#if QRK_HQC_DEDUPE_CF
+  dedupe_wave_cf<WT>(s);
+#else
+  dedupe_wave_loop<WT>(s);
+#endif
+}
+
+// QRK_HQC_GDOUBLED: 1 the doubled operands are built straight from global words in the staging
+// phase (3 loads per word: 2-3 % slower); 0 raw words are staged in LDS first (default)
+#ifndef QRK_HQC_GDOUBLED
+#define QRK_HQC_GDOUBLED 0
+#endif
 
 // doubled dense operand: D[q] = raw[q] ^ (clean << n)[q], raw words via rd(j) (0 outside [0, NW32)),
 // clean = raw masked to n bits.  Written for q in [0, NH2).
@@ -384,11 +453,24 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
     const uint32_t v = rd(j);
     return j == P::NW32 - 1 ? (v & TOPMASK) : v;
   };
-#pragma unroll 4
-  for (int q = threadIdx.x; q < P::NH2; q += P::TPB) {
-    uint32_t v = q < P::NW32 ? rd(q) : 0u;
-    if (q >= P::N32) v ^= alignbit(clean(q - P::N32), clean(q - P::N32 - 1), 32 - P::NR);
-    D[q] = v;
+  // every read first, then the stores: with a global-memory reader the thread's loads are all
+  // in flight together (one round trip instead of one per output word)
+  constexpr int QPT = (P::NH2 + P::TPB - 1) / P::TPB;
+  uint32_t d[QPT];
+#pragma unroll
+  for (int k = 0; k < QPT; ++k) {
+    const int q = (int)threadIdx.x + k * P::TPB;
+    uint32_t v = 0;
+    if (q < P::NH2) {
+      v = q < P::NW32 ? rd(q) : 0u;
+      if (q >= P::N32) v ^= alignbit(clean(q - P::N32), clean(q - P::N32 - 1), 32 - P::NR);
+    }
+    d[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < QPT; ++k) {
+    const int q = (int)threadIdx.x + k * P::TPB;
+    if (q < P::NH2) D[q] = d[k];
   }
 }
 
@@ -478,7 +560,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   using P = HQ<L>;
   __shared__ uint32_t D[P::NH2];
   __shared__ uint32_t MB[P::MBW];
-  __shared__ uint32_t SS[2 * P::WMAX], PJ[2 * P::W];
+  __shared__ uint32_t SS[2 * P::WMAX];
   uint32_t* const SX = SS;
   uint32_t* const SY = SS + P::WMAX;
   const size_t hs = blockIdx.x;
@@ -494,7 +576,9 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   // sk = sk_seed || sigma || pk_seed || s  (the coins' first 80 + K bytes, in order)
   for (int j = t; j < (P::KPC + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::KPC);
   __syncthreads();
-  dedupe_wg<L, 2, P::W>(SS, PJ);
+  if (t < 64) dedupe_wave<P::W>(SX);
+  else if (t < 128) dedupe_wave<P::W>(SY);
+  __syncthreads();
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D};
   sparse_dense<L, 1, P::WPT, P::NBT>(SY, P::W, Ds, acc);
@@ -514,6 +598,34 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint6
   for (int b = t; b < P::PK; b += P::TPB) po[b] = mb[SEED + P::K + b];
 }
 
+// ---------------------------------------------------------------- phase trace (tools only)
+// -DQRK_HQC_TRACE=1: workgroup QRK_HQC_TRACE_WG of k_hqc_enc_mul / k_hqc_decode stamps the 100 MHz
+// wall clock at its phase boundaries (tools/hqc_trace.py reads them through qrk_dbg_hqc_trace).
+#ifndef QRK_HQC_TRACE
+#define QRK_HQC_TRACE 0
+#endif
+#ifndef QRK_HQC_TRACE_WG
+#define QRK_HQC_TRACE_WG 30000
+#endif
+#if QRK_HQC_TRACE
+__device__ unsigned long long g_hqc_trace[32];
+#define HQ_MARK(i)                                                                 \
+  do {                                                                             \
+    if (blockIdx.x == QRK_HQC_TRACE_WG && threadIdx.x == 0) g_hqc_trace[i] = wall_clock64(); \
+  } while (0)
+#define HQ_MARK_T(i, tid)                                                          \
+  do {                                                                             \
+    if (blockIdx.x == QRK_HQC_TRACE_WG && threadIdx.x == (tid)) g_hqc_trace[i] = wall_clock64(); \
+  } while (0)
+#else
+#define HQ_MARK_T(i, tid) \
+  do {                    \
+  } while (0)
+#define HQ_MARK(i) \
+  do {             \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- Encaps / re-encryption
 // Encaps (REENC = false): m, salt from coins; s from pk; writes ct and the K-hash message rows.
 // Decaps re-encryption (REENC = true): m' from mp; s and sigma from sk; compares (u', v') with the
@@ -527,12 +639,13 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2], D2[P::NH2];
   __shared__ __attribute__((aligned(16))) uint32_t MB[P::MBW];
-  __shared__ uint32_t SS[3 * P::WMAX], PJ[3 * P::WR];
+  __shared__ uint32_t SS[3 * P::WMAX];
   uint32_t* const S1 = SS;
   uint32_t* const S2 = SS + P::WMAX;
   uint32_t* const SE = SS + 2 * P::WMAX;
   static_assert(P::WR == P::WE, "one dedupe over r1, r2, e");
-  __shared__ uint8_t GE[512], GL[256], SYM[128], MM[32];
+  __shared__ __attribute__((aligned(4))) uint8_t GE[512], GL[256];
+  __shared__ uint8_t SYM[128], MM[32];
   __shared__ uint32_t DIFF;
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
@@ -540,19 +653,63 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   const uint64_t* rw = row + hs * P::ROWW;
   uint8_t* mb = (uint8_t*)MB;
   const uint8_t* spk = REENC ? sk + hs * P::SK + SEED + P::K : pk + hs * P::PK;  // the pk
-  // phase A: h doubled, s staged (bytes), supports, m, GF tables
+  HQ_MARK(0 + 8 * REENC);
+  // phase A: the global reads of the handshake (doubled h and s, supports, m, GF tables), each
+  // thread's loads issued before any is used
   const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
+  // h and s doubled (s keeps stray bits of a malformed pk)
+#if QRK_HQC_GDOUBLED
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });
-  for (int j = t; j < P::NW32; j += P::TPB) MB[j] = ld32_masked(spk + SEED, j, P::NB);
-  supports_raw<L>(rw, P::WR, S1);
-  supports_raw<L>(rw + P::RWR, P::WR, S2);
-  supports_raw<L>(rw + 2 * P::RWR, P::WE, SE);
-  fill_gf(GE, GL);
-  if (t < P::K) MM[t] = REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t];
+  build_doubled<L>(D2, [&](int j) { return ld32_masked(spk + SEED, j, P::NB); });
+#else
+  static_assert(2 * P::NW32 <= P::MBW, "raw h and s words fit the message buffer");
+  {
+    constexpr int WPT_A = (P::NW32 + P::TPB - 1) / P::TPB;
+    uint32_t hr[WPT_A], sr[WPT_A];
+#pragma unroll
+    for (int k = 0; k < WPT_A; ++k) {
+      const int j = t + k * P::TPB;
+      hr[k] = j < P::NW32 ? h32[j] : 0u;
+      sr[k] = j < P::NW32 ? ld32_masked(spk + SEED, j, P::NB) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < WPT_A; ++k) {
+      const int j = t + k * P::TPB;
+      if (j < P::NW32) {
+        MB[j] = sr[k];
+        MB[P::NW32 + j] = j == P::NW32 - 1 ? hr[k] & ((1u << P::NR) - 1) : hr[k];
+      }
+    }
+  }
+#endif
+  {
+    const uint32_t* r32 = (const uint32_t*)rw;
+    const uint32_t q1 = t < P::WR ? r32[t] : 0u;
+    const uint32_t q2 = t < P::WR ? r32[2 * P::RWR + t] : 0u;
+    const uint32_t qe = t < P::WE ? r32[4 * P::RWR + t] : 0u;
+    const uint32_t ge = t < 128 ? ((const uint32_t*)GF.exp)[t] : 0u;
+    const uint32_t gl = t < 64 ? ((const uint32_t*)GF.log)[t] : 0u;
+    const uint8_t mm = t < P::K ? (REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t]) : 0;
+    if (t < P::WR) S1[t] = (uint32_t)t + __umulhi(q1, (uint32_t)(P::N - t));
+    if (t < P::WR) S2[t] = (uint32_t)t + __umulhi(q2, (uint32_t)(P::N - t));
+    if (t < P::WE) SE[t] = (uint32_t)t + __umulhi(qe, (uint32_t)(P::N - t));
+    if (t < 128) ((uint32_t*)GE)[t] = ge;
+    if (t < 64) ((uint32_t*)GL)[t] = gl;
+    if (t < P::K) MM[t] = mm;
+  }
   if (t == 0) DIFF = 0;
   __syncthreads();
-  // phase B: s doubled (keeps stray bits of a malformed pk), RS parity, dedupe
+  HQ_MARK(1 + 8 * REENC);
+  // phase B: RS parity (wave 3), the three duplicate removals on waves 0-2
+#if !QRK_HQC_GDOUBLED
+  build_doubled<L>(D1, [&](int j) { return MB[P::NW32 + j]; });
   build_doubled<L>(D2, [&](int j) { return MB[j]; });
+#endif
+  HQ_MARK_T(24 + 4 * REENC, 0);
+  if (wave == 0) dedupe_wave<P::WR>(S1);
+  HQ_MARK_T(25 + 4 * REENC, 0);
+  if (wave == 1) dedupe_wave<P::WR>(S2);
+  if (wave == 2) dedupe_wave<P::WE>(SE);
   if (wave == 3) {
     const RsTab<L>& rs = rs_tab<L>();
     if (lane < P::T2) {
@@ -569,17 +726,22 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
     }
     if (lane + 64 < P::N1) SYM[lane + 64] = MM[lane + 64 - P::T2];
   }
-  dedupe_wg<L, 3, P::WR>(SS, PJ);  // ends with a barrier
+  HQ_MARK_T(26 + 4 * REENC, 192);
+  __syncthreads();
+  HQ_MARK(2 + 8 * REENC);
   // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
   uint32_t acc[2][P::WPTE] = {};
   const uint32_t* const Ds[2] = {D1, D2};
   sparse_dense<L, 2, P::WPTE, P::NBTE>(S2, P::WR, Ds, acc);
+  HQ_MARK(3 + 8 * REENC);
   __syncthreads();
+  HQ_MARK(4 + 8 * REENC);
   uint32_t* const outs[2] = {D1, D2};
   prod_combine<2, P::WPTE, P::NBTE>(outs, acc, [&] {
     for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
     for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
   });
+  HQ_MARK(5 + 8 * REENC);
   constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
   constexpr int UOFF = P::K / 4;  // u at message byte K
   auto vword = [&](int j) {       // v word j = (r2 s + e + codeword) word j
@@ -617,6 +779,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   }
   for (int b = P::MSGB + t; b < 8 * P::MW; b += P::TPB) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
   __syncthreads();
+  HQ_MARK(6 + 8 * REENC);
   // phase E: K-hash message rows (aligned words), ciphertext bytes
   const uint64_t* m64 = (const uint64_t*)MB;
   uint64_t* mo = msg + hs * P::MW;
@@ -627,6 +790,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
     for (int b = t; b < P::NB + P::VB; b += P::TPB) co[b] = mb[P::K + b];
     if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
   }
+  HQ_MARK(7 + 8 * REENC);
 }
 
 // Hadamard butterfly on lane bit BIT for two symbols (x0 / x1 = positions l / l + 64):
@@ -684,7 +848,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   __shared__ uint32_t D1[P::NH2];
   __shared__ uint32_t T[P::NWP];
   __shared__ uint32_t MB[(P::NB + P::VB + 8) / 4 + 1];
-  __shared__ uint32_t SY[P::WMAX], PJ[P::W];
+  __shared__ uint32_t SY[P::WMAX];
   __shared__ uint8_t SYM[128];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
@@ -692,17 +856,31 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   const uint64_t* rw = row + hs * P::ROWW;
   uint8_t* mb = (uint8_t*)MB;
   const uint8_t* c = ct + hs * P::CT;
+  HQ_MARK(16);
+  // u doubled straight from the ct's u words (bits >= n as received; the word straddling into v is
+  // cut), u || v bytes staged, supports -- all of the handshake's global reads before the barrier
+  constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
+  constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+#if QRK_HQC_GDOUBLED
+  build_doubled<L>(D1, [&](int j) {
+    const uint32_t w = ld32_masked(c, j, P::NB + P::VB);
+    return j == P::NW32 - 1 ? (w & BM) : w;
+  });
+#endif
   for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::NB + P::VB);
   supports_raw<L>(rw + P::RWW, P::W, SY);
   __syncthreads();
-  // u doubled: raw words = the ct's u bytes (bits >= n as received); the word straddling into v is cut
-  constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
-  constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+#if !QRK_HQC_GDOUBLED
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? (MB[j] & BM) : MB[j]; });
-  dedupe_wg<L, 1, P::W>(SY, PJ);
+#endif
+  HQ_MARK(17);
+  if (wave == 0) dedupe_wave<P::W>(SY);
+  __syncthreads();
+  HQ_MARK(18);
   uint32_t acc[1][P::WPT] = {};
   const uint32_t* const Ds[1] = {D1};
   sparse_dense<L, 1, P::WPT, P::NBT>(SY, P::W, Ds, acc);
+  HQ_MARK(19);
   // T = v - u y (words >= VW32 zero): fold v into class 0's partial sums, then combine
   if (t < P::NBT) {
     const int j0 = t * P::WPT;
@@ -718,6 +896,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
   }
   uint32_t* const outs[1] = {T};
   prod_combine<1, P::WPT, P::NBT>(outs, acc, [] {});
+  HQ_MARK(20);
   // duplicated RM(1,7): one wave per symbol pair (two independent chains interleave), lane l
   // holds positions l and l + 64 of each symbol; the Hadamard butterflies exchange through DPP
   // and v_permlane16/32_swap (no LDS round trips), the first maximum is a DPP + readlane max
@@ -756,7 +935,9 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
     }
   }
   __syncthreads();
+  HQ_MARK(21);
   if (t < P::N1) syms[hs * sym_stride + t] = SYM[t];
+  HQ_MARK(22);
 }
 
 // wave-scope LDS ordering (the wave's lanes exchange through LDS)
@@ -887,12 +1068,13 @@ template <int L, int WT>
 __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_supports(size_t n, const uint32_t* __restrict__ r,
                                                       uint32_t* __restrict__ sup) {
   using P = HQ<L>;
-  __shared__ uint32_t SS[P::WMAX], PJ[WT];
+  __shared__ uint32_t SS[P::WMAX];
   const size_t v = blockIdx.x;
   if (v >= n) return;
   for (int i = threadIdx.x; i < WT; i += P::TPB) SS[i] = (uint32_t)i + __umulhi(r[v * WT + i], (uint32_t)(P::N - i));
   __syncthreads();
-  dedupe_wg<L, 1, WT>(SS, PJ);
+  if (threadIdx.x < 64) dedupe_wave<WT>(SS);  // the product kernels' duplicate removal
+  __syncthreads();
   for (int i = threadIdx.x; i < WT; i += P::TPB) sup[v * WT + i] = SS[i];
 }
 
@@ -1051,3 +1233,9 @@ hipError_t hqc_decaps(const AlgInfo& a, size_t n, uint8_t* ss, const uint8_t* ct
 }
 
 }  // namespace qrk
+
+#if QRK_HQC_TRACE
+extern "C" int qrk_dbg_hqc_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(qrk::hqc::g_hqc_trace), sizeof(qrk::hqc::g_hqc_trace)) == hipSuccess ? 0 : -1;
+}
+#endif

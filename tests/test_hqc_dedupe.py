@@ -1,6 +1,8 @@
-"""The closed form of HQC's duplicate removal that the HIP kernels use (csrc/hqc.hip
-dedupe_wg), checked on the CPU against the spec's serial loop (oracle/py/hqc_spec.py
-remove_duplicates, restating vect_set_random_fixed_weight of the 2023-04-30 HQC).
+"""HQC's duplicate removal as the HIP kernels run it (csrc/hqc.hip dedupe_wave: one wave per
+vector, element 64e + l in lane l's register e, one v_readlane broadcast and one ballot per
+register per step, masked to j > i), checked on the CPU against the spec's serial loop
+(oracle/py/hqc_spec.py remove_duplicates, restating vect_set_random_fixed_weight of the
+2023-04-30 HQC).  Also kept: the round-1 closed form (pointer jumping over the workgroup).
 
 Serial loop: for i = w-2 .. 0, s_i := i when s_i equals some s_j with j > i.
 Closed form: s_i is replaced iff (s_j == s_i for some j > i, original values) or
@@ -41,6 +43,28 @@ def closed_form(s, order_rng=None):
     return [i if rep[i] else s[i] for i in range(w)]
 
 
+def wave_form(s):
+    """dedupe_wave restated: registers v[e][lane], ballots as 64-bit masks."""
+    w = len(s)
+    ne = (w + 63) // 64
+    sentinel = 0xFFFFFFFF
+    v = [[s[64 * e + l] if 64 * e + l < w else sentinel for l in range(64)] for e in range(ne)]
+    for i in range(w - 2, -1, -1):
+        ei, li = i >> 6, i & 63
+        si = v[ei][li]  # v_readlane
+        hit = 0
+        for e in range(ne):
+            if 64 * e + 63 <= i:
+                continue
+            m = sum(1 << l for l in range(64) if v[e][l] == si)  # ballot
+            if 64 * e <= i:
+                m &= (~0 << (i - 64 * e + 1)) & ((1 << 64) - 1)
+            hit |= m
+        if hit:
+            v[ei][li] = i
+    return [v[i >> 6][i & 63] for i in range(w)]
+
+
 def crafted(rng, w, n, kind):
     if kind == "narrow":  # s_i in [i, i + 3]: many value and index collisions
         return [i + rng.randrange(4) for i in range(w)]
@@ -53,13 +77,14 @@ def crafted(rng, w, n, kind):
     return [rng.randrange(i, n) for i in range(w)]
 
 
-@pytest.mark.parametrize("w", [2, 3, 5, 64, 66, 75, 100, 114, 131, 149])
+@pytest.mark.parametrize("w", [2, 3, 5, 63, 64, 65, 66, 75, 100, 114, 128, 129, 131, 149, 192])
 @pytest.mark.parametrize("kind", ["narrow", "same", "chain", "small", "full"])
 def test_closed_form_matches_serial_loop(w, kind):
     rng = random.Random(w * 31 + len(kind))
     for trial in range(12):
         s = crafted(rng, w, 57637, kind)
         want = H.remove_duplicates(s)
+        assert wave_form(s) == want
         assert closed_form(s) == want
         assert closed_form(s, order_rng=rng) == want
         assert len(set(want)) == w  # the result is a support: distinct positions
@@ -71,4 +96,4 @@ def test_fixed_weight_support_uses_the_loop():
     raw = se2.read(4 * 75)
     r = [int.from_bytes(raw[4 * i:4 * i + 4], "little") for i in range(75)]
     s = [i + ((r[i] * (17669 - i)) >> 32) for i in range(75)]
-    assert H.fixed_weight_support(se, 17669, 75) == H.remove_duplicates(s) == closed_form(s)
+    assert H.fixed_weight_support(se, 17669, 75) == H.remove_duplicates(s) == closed_form(s) == wave_form(s)
