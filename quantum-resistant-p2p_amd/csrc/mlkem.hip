@@ -1396,7 +1396,12 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
 #ifndef QRK_SMALL_MAX
 #define QRK_SMALL_MAX 256
 #endif
-constexpr int ONE_WAVES = 12;  // 3 waves per SIMD: the 16-lane cores fit in 170 VGPRs
+constexpr int ONE_WAVES = 12;  // Encaps / Decaps: 3 waves per SIMD, the 16-lane cores fit in 170 VGPRs
+#ifndef QRK_KG_WAVES
+#define QRK_KG_WAVES 16  // KeyGen (88 VGPRs): every PRF and SampleNTT item of ML-KEM-768 on its own wave
+#endif
+constexpr int KG_WAVES = QRK_KG_WAVES;
+constexpr int MAX_ONE_WAVES = KG_WAVES > ONE_WAVES ? KG_WAVES : ONE_WAVES;
 
 // ordering between lanes of one wave across phases: a workgroup-scope release / acquire around
 // a wave barrier
@@ -1521,7 +1526,7 @@ struct OneLds {
   uint64_t ps[PRF_W * 16];       // PRF outputs (2K + 1 <= 9)
   uint32_t bop[4][16][16];       // NTT(y_j) / NTT(s_j) as basemul operands: word w of lane L at [j][w][L]
   float ef[4][16][16];           // KeyGen: NTT(e_i), coefficient t of lane L at [i][t][L]
-  uint32_t pbuf[ONE_WAVES][44];  // per-wave SampleNTT parse buffers
+  uint32_t pbuf[MAX_ONE_WAVES][44];  // per-wave SampleNTT parse buffers
   uint64_t io[600];              // the handshake's inputs (Encaps ek | m, Decaps c | dk; KeyGen ek)
   uint64_t seed[4], mp[4], kp[4], kb[4];
   uint32_t diff[8];              // Decaps compare: per worker group
@@ -1533,11 +1538,12 @@ struct OneLds {
 // workgroups); every thread of the workgroup calls it.  With a completion flag (single-shot host
 // calls) the outputs are first made visible at system scope, then the flag is stored.
 __device__ __forceinline__ void wipe_one(OneLds& sl, uint32_t* done, uint32_t ticket) {
+  const int nthreads = (int)blockDim.x;
   if (done) __threadfence_system();
   __syncthreads();
   if (done && threadIdx.x == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   uint4* w = (uint4*)&sl;
-  for (int x = threadIdx.x; x < (int)(sizeof(OneLds) / 16); x += 64 * ONE_WAVES) w[x] = make_uint4(0, 0, 0, 0);
+  for (int x = threadIdx.x; x < (int)(sizeof(OneLds) / 16); x += nthreads) w[x] = make_uint4(0, 0, 0, 0);
 }
 
 // Cross-wave flags (Decaps, where the J chain must not hold a workgroup barrier): a wave's LDS
@@ -1555,7 +1561,7 @@ __device__ __forceinline__ void one_wait(int* p, int target) {
 // Copy one handshake's inputs (host-mapped or device memory) into LDS in one parallel burst: the
 // zero-copy single-shot calls then pay one PCIe round trip instead of one per dependent load.
 __device__ __forceinline__ void stage_in(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, int words) {
-  for (int w = threadIdx.x; w < words; w += 64 * ONE_WAVES) dst[w] = src[w];
+  for (int w = threadIdx.x; w < words; w += (int)blockDim.x) dst[w] = src[w];
 }
 
 __device__ __forceinline__ void bop_store(OneLds& sl, int j, const BOp& b, int L) {
@@ -1823,7 +1829,7 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
 }
 
 template <int K>
-__global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const uint8_t* __restrict__ coins,
+__global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const uint8_t* __restrict__ coins,
                                                                 uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
                                                                 uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
@@ -1852,7 +1858,7 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_keygen_one(size_t n, const u
   }
   __syncthreads();
 #pragma unroll 1
-  for (int it = wave; it < 2 * K + K * K; it += ONE_WAVES) {  // the 2K PRFs (+ NTTs) first, then SampleNTT
+  for (int it = wave; it < 2 * K + K * K; it += KG_WAVES) {  // the 2K PRFs (+ NTTs) first, then SampleNTT
     if (it < 2 * K)
       prf_ntt_one<K, true>(sl, it, dk, c);
     else
@@ -1931,7 +1937,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_keygen_one", s.main, k_keygen_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, coins,
+    QRK_LAUNCH("k_keygen_one", s.main, k_keygen_one<K>, dim3((unsigned)n), dim3(64 * KG_WAVES), 0, s.main, n, coins,
                pk, sk, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }

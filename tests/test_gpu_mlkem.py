@@ -126,6 +126,40 @@ def test_single_shot_oqs_api():
     assert oqs.KeyEncapsulation(alg, k.export_secret_key()).decap_secret(c2) == s2
 
 
+@pytest.mark.parametrize("alg", ALGS)
+def test_single_shot_paths_all_params(alg):
+    """The n = 1 one-launch kernels through the OQS API (zero-copy pinned I/O, completion flag):
+    byte-exact KeyGen / Encaps / Decaps, implicit rejection of a tampered ciphertext (ss = J(z || c)
+    from the oracle), and the FIPS 203 modulus check raising RuntimeError, repeated so the flag
+    tickets and the reused pinned mirror are exercised."""
+    import oracle as orc
+    from qrkem import oqs
+    rng = np.random.default_rng(sum(map(ord, alg)))
+    for it in range(4):
+        kc = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+        ec = rng.integers(0, 256, 32, dtype=np.uint8).tobytes()
+        k = oqs.KeyEncapsulation(alg)
+        pk = k.generate_keypair_derand(kc)
+        sk = k.export_secret_key()
+        opk, osk = orc.keypair(alg, kc)
+        assert pk == opk and sk == osk
+        c, ss = oqs.KeyEncapsulation(alg).encap_secret_derand(pk, ec)
+        oc, oss = orc.encaps(alg, pk, ec)
+        assert c == oc and ss == oss
+        assert oqs.KeyEncapsulation(alg, sk).decap_secret(c) == oss
+        bad = bytearray(c)
+        bad[(17 * it) % len(bad)] ^= 1 << it
+        want = orc.batch_decaps(alg, np.frombuffer(sk, np.uint8).reshape(1, -1),
+                                np.frombuffer(bytes(bad), np.uint8).reshape(1, -1))[0].tobytes()
+        got = oqs.KeyEncapsulation(alg, sk).decap_secret(bytes(bad))
+        assert got == want and got != oss
+    badpk = bytearray(pk)
+    badpk[0] = 0xFF
+    badpk[1] |= 0x0F  # first coefficient 4095 >= q
+    with pytest.raises(RuntimeError):
+        oqs.KeyEncapsulation(alg).encap_secret(bytes(badpk))
+
+
 def test_bench_coins_device_matches_oracle(engines):
     import oracle as orc
     eng = engines["ML-KEM-768"]

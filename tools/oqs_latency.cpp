@@ -17,7 +17,7 @@ static double med(std::vector<double>& v) {
 
 int main(int argc, char** argv) {
   const char* alg = argc > 1 ? argv[1] : "ML-KEM-768";
-  const int N = 400;
+  const int N = argc > 2 ? atoi(argv[2]) : 400;
   OQS_KEM* kem = OQS_KEM_new(alg);
   if (!kem) return 1;
   std::vector<uint8_t> pk(kem->length_public_key), sk(kem->length_secret_key), ct(kem->length_ciphertext),
