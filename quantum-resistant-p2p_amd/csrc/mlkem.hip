@@ -1393,8 +1393,10 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
 //   keygen: wave 0 G(d || k), then PRFs and SampleNTT over all waves, the core, H(ek)
 // then the 2K+1 (2K) PRFs, one per wave, and the 16-lane polynomial core.  SampleNTT entries, PRF
 // outputs and the decaps intermediates stay in LDS (the batched layouts at tile width 16, C = 1).
+// One launch per operation wins up to 1024 handshakes (ML-KEM-768 encaps+decaps 249 against 346 us
+// at 1024, 466 against 396 at 2048: profiles/r2/small_crossover.json)
 #ifndef QRK_SMALL_MAX
-#define QRK_SMALL_MAX 256
+#define QRK_SMALL_MAX 1024
 #endif
 constexpr int ONE_WAVES = 12;  // Encaps / Decaps: 3 waves per SIMD, the 16-lane cores fit in 170 VGPRs
 #ifndef QRK_KG_WAVES

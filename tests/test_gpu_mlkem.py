@@ -32,7 +32,7 @@ def _host(t):
 
 
 @pytest.mark.parametrize("alg", ALGS)
-@pytest.mark.parametrize("n", [1, 17, 255, 256, 257, 301])
+@pytest.mark.parametrize("n", [1, 17, 255, 256, 257, 301, 1024, 1025])
 def test_roundtrip_matches_oracle(engines, alg, n):
     """n <= 256 runs the one-launch small-batch kernels (k_*_small), n > 256 the batched
     schedule; both byte-exact vs the oracle, including the boundary."""
