@@ -24,9 +24,29 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
+// a | b and a ^ (~b & c) pinned to full-rate encodings (the compiler would otherwise fold a
+// preceding shift into the half-rate v_lshl_or_b32, or split chi into v_bfi + v_xor)
+__device__ __forceinline__ uint32_t or32(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_or_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t chi3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd2" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 struct u2 {
   uint32_t lo, hi;
 };
+
+// QRK_KECCAK_SHIFT64 1: a rotation is one 64-bit shift (v_lshlrev_b64 / v_lshrrev_b64 yields
+// one half of the result exactly) + one 32-bit shift + one OR for the other half, in place of
+// two half-rate v_alignbit_b32 (tools/rot64_probe.hip).
+#ifndef QRK_KECCAK_SHIFT64
+#define QRK_KECCAK_SHIFT64 0
+#endif
 
 template <int N>
 __device__ __forceinline__ u2 rol(u2 x) {
@@ -34,11 +54,23 @@ __device__ __forceinline__ u2 rol(u2 x) {
     return x;
   } else if constexpr (N == 32) {
     return {x.hi, x.lo};
+#if QRK_KECCAK_SHIFT64
+  } else if constexpr (N < 32) {
+    uint64_t t;
+    asm("v_lshlrev_b64 %0, %2, %1" : "=v"(t) : "v"(((uint64_t)x.hi << 32) | x.lo), "i"(N));
+    return {or32((uint32_t)t, x.hi >> (32 - N)), (uint32_t)(t >> 32)};
+  } else {
+    uint64_t t;
+    asm("v_lshrrev_b64 %0, %2, %1" : "=v"(t) : "v"(((uint64_t)x.hi << 32) | x.lo), "i"(64 - N));
+    return {(uint32_t)t, or32((uint32_t)(t >> 32), x.lo << (N - 32))};
+  }
+#else
   } else if constexpr (N < 32) {
     return {__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - N), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - N)};
   } else {
     return {__builtin_amdgcn_alignbit(x.hi, x.lo, 64 - N), __builtin_amdgcn_alignbit(x.lo, x.hi, 64 - N)};
   }
+#endif
 }
 
 __constant__ static const uint32_t KRC_LO[24] = {
@@ -111,8 +143,13 @@ __device__ __forceinline__ void keccak_f(KState& s) {
 #pragma unroll
       for (int x = 0; x < 5; ++x) {
         const u2 b0 = B[x + 5 * y], b1 = B[(x + 1) % 5 + 5 * y], b2 = B[(x + 2) % 5 + 5 * y];
+#if QRK_KECCAK_SHIFT64
+        s.a[x + 5 * y].lo = chi3(b0.lo, b1.lo, b2.lo);
+        s.a[x + 5 * y].hi = chi3(b0.hi, b1.hi, b2.hi);
+#else
         s.a[x + 5 * y].lo = b0.lo ^ (~b1.lo & b2.lo);
         s.a[x + 5 * y].hi = b0.hi ^ (~b1.hi & b2.hi);
+#endif
       }
     s.a[0].lo ^= KRC_LO[r];
     s.a[0].hi ^= KRC_HI[r];

@@ -236,6 +236,11 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #ifndef QRK_XOF_CMP
 #define QRK_XOF_CMP 1
 #endif
+// QRK_XOF_ACC 1: SampleNTT acceptance as a shifted difference (compact_block below); A/B on one
+// box no faster than v_cmp + v_cndmask (profiles/r2/ab_xof_acc_rejected.jsonl), kept as an option
+#ifndef QRK_XOF_ACC
+#define QRK_XOF_ACC 0
+#endif
 #ifndef QRK_ENC_PREFETCH
 #define QRK_ENC_PREFETCH 1
 #endif
@@ -261,6 +266,46 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 // `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
 // 8-11 are zero, so an entry address is one v_bitop3_b32, (pos & 0xF00) | rb, with the static
 // LDS base folded into the ds_write offset.
+#if QRK_XOF_ACC
+// Ring layout with a 512-B entry stride: the two waves of a pair interleave their 256-B entry
+// rows (wave & 1 selects the half), so the ring is still 16 KB per 4-wave workgroup.  The
+// running position is kept as P = 511 (cnt + 1): an accepted candidate adds
+// (uint)(c - q) >> 23 = 511 (c < q) or 0 (c >= q) -- two full-rate ops in place of the
+// v_cmp + v_cndmask pair (about three issue slots, profiles/r1/valu_peak_r1b.json) -- and
+// P >> 9 = cnt for every cnt <= 511, so bits 9-12 of P index the ring entry directly.
+template <int TW = 64>
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
+  const uint32_t* ring = (const uint32_t*)(ring_all + rb);
+  uint32_t P = 511u * (uint32_t)(cnt + 1);
+#pragma unroll
+  for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
+    uint32_t d[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const int di = 3 * t + e;
+      d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
+    }
+    int c[8];
+    split12(d[0], d[1], d[2], c);
+    const int before = (int)(P >> 9);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      *(uint32_t*)(ring_all + and_or3(P, 0x1E00u, rb)) = (uint32_t)c[e];
+      P += (uint32_t)(c[e] - Q) >> 23;
+    }
+    const int now = (int)(P >> 9);
+    const int ch = before >> 3;
+    if ((now >> 3) != ch && ch < 32) {
+      const uint32_t* r = ring + (ch & 1) * 8 * 128;
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 128], 16, r[(2 * j) * 128]);
+      dst[ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+  cnt = (int)(P >> 9);
+}
+#else
 template <int TW = 64>
 __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
@@ -302,6 +347,8 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
   }
 }
 
+#endif
+
 // FIX == false: every entry squeezes exactly 3 blocks (uniform across the
 // wave); the ~0.7% that still lack 256 values append their index to `fix`.
 // FIX == true: one lane per listed entry recomputes it with as many blocks as
@@ -334,7 +381,11 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
                                              size_t n, size_t C, uint4* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
+#if QRK_XOF_ACC
+  const uint32_t rb = (threadIdx.x >> 7) * 8192 + ((threadIdx.x >> 6) & 1) * 256 + (threadIdx.x & 63) * 4;
+#else
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;
+#endif
   const size_t stride = FIX ? (size_t)gridDim.x * 256 : 0;
   size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t limit = FIX ? (size_t)*nfix : (size_t)K * K * C;
