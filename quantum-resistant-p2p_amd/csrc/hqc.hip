@@ -319,12 +319,25 @@ __global__ __launch_bounds__(256) void k_hqc_hash(const uint64_t* __restrict__ m
 }
 
 // ---------------------------------------------------------------- workgroup / hs helpers
+// Thread index as seen by the workgroup helpers: threadIdx.x plus an opaque zero produced inside
+// the caller's code (a volatile v_mov).  In the persistent handshake loop (k_hqc_enc_mul) the
+// compiler would otherwise hoist every loop-invariant LDS address out of the loop and keep it
+// live in a register (110-180 VGPRs, then spills under an occupancy bound); derived from this
+// value, the addresses are recomputed per iteration (a few VALU ops) instead.
+__device__ __forceinline__ int hq_tid() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  const int t = (int)threadIdx.x + z;
+  __builtin_assume(t >= 0 && t < 1024);
+  return t;
+}
+
 // support of a fixed-weight vector from its random words: s_i = i + floor(r_i (n - i) / 2^32)
 template <int L>
 __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, uint32_t* sup) {
   using P = HQ<L>;
   const uint32_t* r32 = (const uint32_t*)words;
-  for (int i = threadIdx.x; i < weight; i += P::TPB)
+  for (int i = hq_tid(); i < weight; i += P::TPB)
     sup[i] = (uint32_t)i + __umulhi(r32[i], (uint32_t)(P::N - i));
 }
 
@@ -345,7 +358,7 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
   constexpr uint32_t NONE = 0xFFFFu, REP = 0x80000000u;
   constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);
   static_assert(NE <= 3 && WT > 1, "weight");
-  const int lane = threadIdx.x & 63;
+  const int lane = hq_tid() & 63;
   uint32_t v[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
@@ -398,7 +411,7 @@ template <int WT>
 __device__ __forceinline__ void dedupe_wave_loop(uint32_t* s) {
   constexpr int NE = (WT + 63) / 64;
   static_assert(NE <= 3 && WT > 1, "weight");
-  const int lane = threadIdx.x & 63;
+  const int lane = hq_tid() & 63;
   uint32_t v[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
@@ -456,10 +469,11 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   // every read first, then the stores: with a global-memory reader the thread's loads are all
   // in flight together (one round trip instead of one per output word)
   constexpr int QPT = (P::NH2 + P::TPB - 1) / P::TPB;
+  const int tq = hq_tid();
   uint32_t d[QPT];
 #pragma unroll
   for (int k = 0; k < QPT; ++k) {
-    const int q = (int)threadIdx.x + k * P::TPB;
+    const int q = tq + k * P::TPB;
     uint32_t v = 0;
     if (q < P::NH2) {
       v = q < P::NW32 ? rd(q) : 0u;
@@ -469,7 +483,7 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   }
 #pragma unroll
   for (int k = 0; k < QPT; ++k) {
-    const int q = (int)threadIdx.x + k * P::TPB;
+    const int q = tq + k * P::TPB;
     if (q < P::NH2) D[q] = d[k];
   }
 }
@@ -481,12 +495,13 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
                                              uint32_t (&acc)[NV][WPT]) {
   using P = HQ<L>;
   constexpr int PC = P::TPB / NBT;
-  const int j0 = (int)(threadIdx.x % NBT) * WPT;
+  const int tt = hq_tid();
+  const int j0 = (tt % NBT) * WPT;
   // one operand: unrolled so the next position's support read and window are in flight together;
   // two operands: not unrolled (both windows already in flight; keeps <= 64 VGPRs, 8 waves / SIMD)
   constexpr int UNR = NV == 1 ? 2 : 1;
 #pragma unroll UNR
-  for (int i = (int)(threadIdx.x / NBT); i < weight; i += PC) {
+  for (int i = tt / NBT; i < weight; i += PC) {
     const uint32_t k = sup[i];
     const uint32_t e = (uint32_t)P::N - k;
     const int off = (int)(e >> 5) + j0;
@@ -507,8 +522,9 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
 // XOR phase (further commutative updates of out).  Ends with a barrier.
 template <int NV, int WPT, int NBT, typename Extra>
 __device__ __forceinline__ void prod_combine(uint32_t* const (&out)[NV], const uint32_t (&acc)[NV][WPT], Extra extra) {
-  const int j0 = (int)(threadIdx.x % NBT) * WPT;
-  const bool first = threadIdx.x < NBT;
+  const int tt = hq_tid();
+  const int j0 = (tt % NBT) * WPT;
+  const bool first = tt < NBT;
   if (first)
 #pragma unroll
     for (int v = 0; v < NV; ++v)
@@ -627,11 +643,88 @@ __device__ unsigned long long g_hqc_trace[32];
 #endif
 
 // ---------------------------------------------------------------- Encaps / re-encryption
+// Persistent workgroups (QRK_HQC_PERSIST 1): a grid of a few workgroups per CU walks the
+// batch (hs = blockIdx.x, + gridDim.x, ...), and each iteration issues the NEXT handshake's global
+// reads (raw h and s words, supports, m) into
+// registers right after its own staging barrier; they land while this handshake's duplicate
+// removal, products and assembly run, taking the ~10 us load phase of a fresh workgroup
+// (profiles/r2/hqc128_phase_trace_*.json) off its critical path.  0 (default): one workgroup
+// per hs, the loop runs once.
+// A/B on one box (profiles/r2/ab_hqc_persist_rejected.jsonl): the persistent form is slower
+// (HQC-128 enc_mul 0.886 vs 0.761 ms, HQC-256 5.96 vs 4.94 ms): with 8 workgroups per CU the fresh
+// workgroups' load phases already overlap the resident ones' work, while the prefetch registers
+// cost spills or occupancy.  Kept as an option, off by default.
+#ifndef QRK_HQC_PERSIST
+#define QRK_HQC_PERSIST 0
+#endif
+#ifndef QRK_HQC_WPE
+#define QRK_HQC_WPE 8
+#endif
+#ifndef QRK_HQC_WG_PER_CU
+#define QRK_HQC_WG_PER_CU 8
+#endif
+
+// word j of a byte string at any alignment, split in two halves: issue() starts the one or two
+// aligned dword loads (no use of the data), finish() combines them -- ld32_masked across a gap
+struct Ld32 {
+  uint32_t w0, w1;
+};
+__device__ __forceinline__ Ld32 ld32_issue(const uint8_t* src, int j, int nbytes) {
+  const uintptr_t a = (uintptr_t)src + 4 * (uintptr_t)j;
+  const uint32_t* b = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  const int valid = nbytes - 4 * j;
+  Ld32 r;
+  r.w0 = b[0];
+  r.w1 = (sh != 0 && valid > 4 - (int)(sh >> 3)) ? b[1] : 0u;
+  return r;
+}
+__device__ __forceinline__ uint32_t ld32_finish(Ld32 r, uint32_t sh, int j, int nbytes) {
+  const int valid = nbytes - 4 * j;
+  const uint32_t w = sh ? alignbit(r.w1, r.w0, sh) : r.w0;
+  return valid >= 4 ? w : (w & ((1u << (8 * valid)) - 1));
+}
+
+// one handshake's global reads for k_hqc_enc_mul, held in registers
+template <int L, bool REENC>
+struct EncIn {
+  using P = HQ<L>;
+  static constexpr int WA = (P::NW32 + P::TPB - 1) / P::TPB;
+  uint32_t h[WA];
+  Ld32 sw[WA];
+  uint32_t q1, q2, qe, mm, ssh;
+};
+
+template <int L, bool REENC>
+__device__ __forceinline__ void enc_issue(EncIn<L, REENC>& in, size_t hs, const uint64_t* __restrict__ row,
+                                          const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
+                                          const uint8_t* __restrict__ mp, const uint8_t* __restrict__ sk) {
+  using P = HQ<L>;
+  const int t = hq_tid();
+  const uint64_t* rw = row + hs * P::ROWW;
+  const uint8_t* spk = REENC ? sk + hs * P::SK + SEED + P::K : pk + hs * P::PK;  // the pk
+  const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
+  in.ssh = (uint32_t)(((uintptr_t)spk + SEED) & 3) * 8;
+#pragma unroll
+  for (int k = 0; k < EncIn<L, REENC>::WA; ++k) {
+    const int j = t + k * P::TPB;
+    in.h[k] = j < P::NW32 ? h32[j] : 0u;
+    in.sw[k] = j < P::NW32 ? ld32_issue(spk + SEED, j, P::NB) : Ld32{0u, 0u};
+  }
+  const uint32_t* r32 = (const uint32_t*)rw;
+  in.q1 = t < P::WR ? r32[t] : 0u;
+  in.q2 = t < P::WR ? r32[2 * P::RWR + t] : 0u;
+  in.qe = t < P::WE ? r32[4 * P::RWR + t] : 0u;
+  in.mm = t < P::K ? (REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t]) : 0u;
+}
+
 // Encaps (REENC = false): m, salt from coins; s from pk; writes ct and the K-hash message rows.
 // Decaps re-encryption (REENC = true): m' from mp; s and sigma from sk; compares (u', v') with the
 // received ct; message = (m' if equal else sigma) || u || v of the received ct; status -1 if unequal.
+// 8 waves per SIMD at HQC-128 as before the loop (<= 64 VGPRs; HQC-192/256 are held to 5 by their
+// LDS): without the bound the compiler keeps loop-invariant values live across the handshake loop
 template <int L, bool REENC>
-__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 128 ? QRK_HQC_WPE : 5))) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
                                                      const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ ct_out, const uint8_t* __restrict__ mp,
                                                      const uint8_t* __restrict__ sk, const uint8_t* __restrict__ ct_in,
@@ -644,153 +737,131 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_enc_mul(size_t n, const uint
   uint32_t* const S2 = SS + P::WMAX;
   uint32_t* const SE = SS + 2 * P::WMAX;
   static_assert(P::WR == P::WE, "one dedupe over r1, r2, e");
+  static_assert(2 * P::NW32 <= P::MBW, "raw h and s words fit the message buffer");
   __shared__ __attribute__((aligned(4))) uint8_t GE[512], GL[256];
   __shared__ uint8_t SYM[128], MM[32];
   __shared__ uint32_t DIFF;
-  const size_t hs = blockIdx.x;
+  size_t hs = blockIdx.x;
   if (hs >= n) return;
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const uint64_t* rw = row + hs * P::ROWW;
   uint8_t* mb = (uint8_t*)MB;
-  const uint8_t* spk = REENC ? sk + hs * P::SK + SEED + P::K : pk + hs * P::PK;  // the pk
-  HQ_MARK(0 + 8 * REENC);
-  // phase A: the global reads of the handshake (doubled h and s, supports, m, GF tables), each
-  // thread's loads issued before any is used
-  const uint32_t* h32 = (const uint32_t*)(rw + 2 * P::RWR + P::RWE);
-  // h and s doubled (s keeps stray bits of a malformed pk)
-#if QRK_HQC_GDOUBLED
-  build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? h32[j] & ((1u << P::NR) - 1) : h32[j]; });
-  build_doubled<L>(D2, [&](int j) { return ld32_masked(spk + SEED, j, P::NB); });
-#else
-  static_assert(2 * P::NW32 <= P::MBW, "raw h and s words fit the message buffer");
-  {
-    constexpr int WPT_A = (P::NW32 + P::TPB - 1) / P::TPB;
-    uint32_t hr[WPT_A], sr[WPT_A];
+  const int t0 = threadIdx.x;
+  if (t0 < 128) ((uint32_t*)GE)[t0] = ((const uint32_t*)GF.exp)[t0];
+  if (t0 < 64) ((uint32_t*)GL)[t0] = ((const uint32_t*)GF.log)[t0];
+  const size_t hstep = QRK_HQC_PERSIST ? gridDim.x : n;
+  EncIn<L, REENC> in;
+  enc_issue<L, REENC>(in, hs, row, coins, pk, mp, sk);
+#pragma unroll 1
+  for (; hs < n; hs += hstep) {
+    const int t = hq_tid(), wave = t >> 6, lane = t & 63;
+    HQ_MARK(0 + 8 * REENC);
+    // phase A: this handshake's reads (issued one iteration earlier) into LDS
 #pragma unroll
-    for (int k = 0; k < WPT_A; ++k) {
-      const int j = t + k * P::TPB;
-      hr[k] = j < P::NW32 ? h32[j] : 0u;
-      sr[k] = j < P::NW32 ? ld32_masked(spk + SEED, j, P::NB) : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < WPT_A; ++k) {
+    for (int k = 0; k < EncIn<L, REENC>::WA; ++k) {
       const int j = t + k * P::TPB;
       if (j < P::NW32) {
-        MB[j] = sr[k];
-        MB[P::NW32 + j] = j == P::NW32 - 1 ? hr[k] & ((1u << P::NR) - 1) : hr[k];
+        MB[j] = ld32_finish(in.sw[k], in.ssh, j, P::NB);
+        MB[P::NW32 + j] = j == P::NW32 - 1 ? in.h[k] & ((1u << P::NR) - 1) : in.h[k];
       }
     }
-  }
-#endif
-  {
-    const uint32_t* r32 = (const uint32_t*)rw;
-    const uint32_t q1 = t < P::WR ? r32[t] : 0u;
-    const uint32_t q2 = t < P::WR ? r32[2 * P::RWR + t] : 0u;
-    const uint32_t qe = t < P::WE ? r32[4 * P::RWR + t] : 0u;
-    const uint32_t ge = t < 128 ? ((const uint32_t*)GF.exp)[t] : 0u;
-    const uint32_t gl = t < 64 ? ((const uint32_t*)GF.log)[t] : 0u;
-    const uint8_t mm = t < P::K ? (REENC ? mp[hs * 32 + t] : coins[hs * P::ENC + t]) : 0;
-    if (t < P::WR) S1[t] = (uint32_t)t + __umulhi(q1, (uint32_t)(P::N - t));
-    if (t < P::WR) S2[t] = (uint32_t)t + __umulhi(q2, (uint32_t)(P::N - t));
-    if (t < P::WE) SE[t] = (uint32_t)t + __umulhi(qe, (uint32_t)(P::N - t));
-    if (t < 128) ((uint32_t*)GE)[t] = ge;
-    if (t < 64) ((uint32_t*)GL)[t] = gl;
-    if (t < P::K) MM[t] = mm;
-  }
-  if (t == 0) DIFF = 0;
-  __syncthreads();
-  HQ_MARK(1 + 8 * REENC);
-  // phase B: RS parity (wave 3), the three duplicate removals on waves 0-2
-#if !QRK_HQC_GDOUBLED
-  build_doubled<L>(D1, [&](int j) { return MB[P::NW32 + j]; });
-  build_doubled<L>(D2, [&](int j) { return MB[j]; });
-#endif
-  HQ_MARK_T(24 + 4 * REENC, 0);
-  if (wave == 0) dedupe_wave<P::WR>(S1);
-  HQ_MARK_T(25 + 4 * REENC, 0);
-  if (wave == 1) dedupe_wave<P::WR>(S2);
-  if (wave == 2) dedupe_wave<P::WE>(SE);
-  if (wave == 3) {
-    const RsTab<L>& rs = rs_tab<L>();
-    if (lane < P::T2) {
-      uint32_t par = 0;
+    if (t < P::WR) S1[t] = (uint32_t)t + __umulhi(in.q1, (uint32_t)(P::N - t));
+    if (t < P::WR) S2[t] = (uint32_t)t + __umulhi(in.q2, (uint32_t)(P::N - t));
+    if (t < P::WE) SE[t] = (uint32_t)t + __umulhi(in.qe, (uint32_t)(P::N - t));
+    if (t < P::K) MM[t] = (uint8_t)in.mm;
+    if (t == 0) DIFF = 0;
+    __syncthreads();
+    HQ_MARK(1 + 8 * REENC);
+    if (QRK_HQC_PERSIST && hs + hstep < n) enc_issue<L, REENC>(in, hs + hstep, row, coins, pk, mp, sk);
+    // phase B: RS parity (wave 3), the three duplicate removals on waves 0-2
+    build_doubled<L>(D1, [&](int j) { return MB[P::NW32 + j]; });
+    build_doubled<L>(D2, [&](int j) { return MB[j]; });
+    HQ_MARK_T(24 + 4 * REENC, 0);
+    if (wave == 0) dedupe_wave<P::WR>(S1);
+    HQ_MARK_T(25 + 4 * REENC, 0);
+    if (wave == 1) dedupe_wave<P::WR>(S2);
+    if (wave == 2) dedupe_wave<P::WE>(SE);
+    if (wave == 3) {
+      const RsTab<L>& rs = rs_tab<L>();
+      if (lane < P::T2) {
+        uint32_t par = 0;
 #pragma unroll
-      for (int i = 0; i < P::K; ++i) {
-        const uint32_t mi = MM[i], lp = rs.lp[i][lane];
-        const uint32_t pr = GE[GL[mi] + lp];
-        par ^= (mi != 0 && lp != 255) ? pr : 0u;
+        for (int i = 0; i < P::K; ++i) {
+          const uint32_t mi = MM[i], lp = rs.lp[i][lane];
+          const uint32_t pr = GE[GL[mi] + lp];
+          par ^= (mi != 0 && lp != 255) ? pr : 0u;
+        }
+        SYM[lane] = (uint8_t)par;
+      } else if (lane < P::T2 + P::K) {
+        SYM[lane] = MM[lane - P::T2];
       }
-      SYM[lane] = (uint8_t)par;
-    } else if (lane < P::T2 + P::K) {
-      SYM[lane] = MM[lane - P::T2];
+      if (lane + 64 < P::N1) SYM[lane + 64] = MM[lane + 64 - P::T2];
     }
-    if (lane + 64 < P::N1) SYM[lane + 64] = MM[lane + 64 - P::T2];
-  }
-  HQ_MARK_T(26 + 4 * REENC, 192);
-  __syncthreads();
-  HQ_MARK(2 + 8 * REENC);
-  // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
-  uint32_t acc[2][P::WPTE] = {};
-  const uint32_t* const Ds[2] = {D1, D2};
-  sparse_dense<L, 2, P::WPTE, P::NBTE>(S2, P::WR, Ds, acc);
-  HQ_MARK(3 + 8 * REENC);
-  __syncthreads();
-  HQ_MARK(4 + 8 * REENC);
-  uint32_t* const outs[2] = {D1, D2};
-  prod_combine<2, P::WPTE, P::NBTE>(outs, acc, [&] {
-    for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
-    for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
-  });
-  HQ_MARK(5 + 8 * REENC);
-  constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
-  constexpr int UOFF = P::K / 4;  // u at message byte K
-  auto vword = [&](int j) {       // v word j = (r2 s + e + codeword) word j
-    const int sym = j / (4 * P::MULT);
-    return D2[j] ^ rm_word(SYM[sym], j & 3);
-  };
-  if constexpr (!REENC) {
-    for (int j = t; j < P::NW32; j += P::TPB) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
-    if (t < P::K) mb[t] = MM[t];
-    __syncthreads();  // the last u word's spare bytes are v's first bytes
-    for (int j = t; j < P::VW32; j += P::TPB) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
-  } else {
-    // received u || v into the message area, then compare with the re-encryption
-    const uint8_t* cin = ct_in + hs * P::CT;
-    static_assert(P::K % 4 == 0, "u || v starts on a word");
-    for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[P::K / 4 + j] = ld32_masked(cin, j, P::NB + P::VB);
+    HQ_MARK_T(26 + 4 * REENC, 192);
     __syncthreads();
-    uint32_t diff = 0;
-    for (int j = t; j < P::NW32; j += P::TPB) {
-      uint32_t u = D1[j], c = MB[UOFF + j];
-      if (j == P::NW32 - 1) {
-        u &= TOPMASK;
-        constexpr int VALID = P::NB - 4 * (P::NW32 - 1);  // bytes of the last word that belong to u
-        constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
-        c &= BM;
+    HQ_MARK(2 + 8 * REENC);
+    // phase C: u = r2 h, v = r2 s (before r1 / e / codeword)
+    uint32_t acc[2][P::WPTE] = {};
+    const uint32_t* const Ds[2] = {D1, D2};
+    sparse_dense<L, 2, P::WPTE, P::NBTE>(S2, P::WR, Ds, acc);
+    HQ_MARK(3 + 8 * REENC);
+    __syncthreads();
+    HQ_MARK(4 + 8 * REENC);
+    uint32_t* const outs[2] = {D1, D2};
+    prod_combine<2, P::WPTE, P::NBTE>(outs, acc, [&] {
+      for (int i = t; i < P::WR; i += P::TPB) atomicXor(&D1[S1[i] >> 5], 1u << (S1[i] & 31));
+      for (int i = t; i < P::WE; i += P::TPB) atomicXor(&D2[SE[i] >> 5], 1u << (SE[i] & 31));
+    });
+    HQ_MARK(5 + 8 * REENC);
+    constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
+    constexpr int UOFF = P::K / 4;  // u at message byte K
+    auto vword = [&](int j) {       // v word j = (r2 s + e + codeword) word j
+      const int sym = j / (4 * P::MULT);
+      return D2[j] ^ rm_word(SYM[sym], j & 3);
+    };
+    if constexpr (!REENC) {
+      for (int j = t; j < P::NW32; j += P::TPB) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
+      if (t < P::K) mb[t] = MM[t];
+      __syncthreads();  // the last u word's spare bytes are v's first bytes
+      for (int j = t; j < P::VW32; j += P::TPB) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
+    } else {
+      // received u || v into the message area, then compare with the re-encryption
+      const uint8_t* cin = ct_in + hs * P::CT;
+      static_assert(P::K % 4 == 0, "u || v starts on a word");
+      for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[P::K / 4 + j] = ld32_masked(cin, j, P::NB + P::VB);
+      __syncthreads();
+      uint32_t diff = 0;
+      for (int j = t; j < P::NW32; j += P::TPB) {
+        uint32_t u = D1[j], c = MB[UOFF + j];
+        if (j == P::NW32 - 1) {
+          u &= TOPMASK;
+          constexpr int VALID = P::NB - 4 * (P::NW32 - 1);  // bytes of the last word that belong to u
+          constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+          c &= BM;
+        }
+        diff |= u ^ c;
       }
-      diff |= u ^ c;
+      for (int j = t; j < P::VW32; j += P::TPB) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
+      if (diff) atomicOr(&DIFF, 1u);
+      __syncthreads();
+      const bool ok = DIFF == 0;
+      if (t < P::K) mb[t] = ok ? MM[t] : sk[hs * P::SK + SEED + t];
+      if (t == 0) status[hs] = ok ? 0 : -1;
     }
-    for (int j = t; j < P::VW32; j += P::TPB) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
-    if (diff) atomicOr(&DIFF, 1u);
+    for (int b = P::MSGB + t; b < 8 * P::MW; b += P::TPB) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
     __syncthreads();
-    const bool ok = DIFF == 0;
-    if (t < P::K) mb[t] = ok ? MM[t] : sk[hs * P::SK + SEED + t];
-    if (t == 0) status[hs] = ok ? 0 : -1;
-  }
-  for (int b = P::MSGB + t; b < 8 * P::MW; b += P::TPB) mb[b] = b == P::MSGB ? 0x05 : (b == P::MSGB + 1 ? 0x1F : 0);
-  __syncthreads();
-  HQ_MARK(6 + 8 * REENC);
-  // phase E: K-hash message rows (aligned words), ciphertext bytes
-  const uint64_t* m64 = (const uint64_t*)MB;
-  uint64_t* mo = msg + hs * P::MW;
-  for (int w = t; w < P::MW; w += P::TPB) mo[w] = m64[w];
-  if constexpr (!REENC) {
-    uint8_t* co = ct_out + hs * P::CT;
+    HQ_MARK(6 + 8 * REENC);
+    // phase E: K-hash message rows (aligned words), ciphertext bytes
+    const uint64_t* m64 = (const uint64_t*)MB;
+    uint64_t* mo = msg + hs * P::MW;
+    for (int w = t; w < P::MW; w += P::TPB) mo[w] = m64[w];
+    if constexpr (!REENC) {
+      uint8_t* co = ct_out + hs * P::CT;
 #pragma unroll 8
-    for (int b = t; b < P::NB + P::VB; b += P::TPB) co[b] = mb[P::K + b];
-    if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
+      for (int b = t; b < P::NB + P::VB; b += P::TPB) co[b] = mb[P::K + b];
+      if (t < SALT) co[P::NB + P::VB + t] = coins[hs * P::ENC + P::K + t];
+    }
+    HQ_MARK(7 + 8 * REENC);
+    __syncthreads();  // the next iteration's staging overwrites MB, SS, MM
   }
-  HQ_MARK(7 + 8 * REENC);
 }
 
 // Hadamard butterfly on lane bit BIT for two symbols (x0 / x1 = positions l / l + 64):
@@ -1091,6 +1162,21 @@ hipError_t supports_t(int kind, size_t n, const uint32_t* r, uint32_t* sup, hipS
 // ---------------------------------------------------------------- launchers
 inline unsigned blocks_for(size_t t) { return (unsigned)((t + 255) / 256); }
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+// grid of a persistent workgroup kernel: as many workgroups as are resident at once (the
+// occupancy query, capped at QRK_HQC_WG_PER_CU per CU), never more than one per handshake.  A
+// workgroup beyond the resident set would only start after a resident one had finished its
+// whole share, so the grid must not exceed it.
+template <typename Kern>
+unsigned wg_grid(size_t n, Kern kern, int tpb) {
+  if (!QRK_HQC_PERSIST) return (unsigned)n;
+  int dev = 0, cus = 256, per = QRK_HQC_WG_PER_CU;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, tpb, 0) == hipSuccess && occ > 0 && occ < per) per = occ;
+  const size_t cap = (size_t)cus * (size_t)per;
+  return (unsigned)(n < cap ? n : cap);
+}
 
 template <int L>
 size_t scratch_t(size_t C) {
@@ -1134,7 +1220,8 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   const size_t C64 = (n + 63) & ~(size_t)63;
   QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, coins,
              (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, C64, v.row);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, coins,
+  static const unsigned genc = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, false>, P::TPB);
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)(n < genc ? n : genc)), dim3(P::TPB), 0, st, n, v.row, coins,
              pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
              v.msg);
   QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
@@ -1157,7 +1244,8 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   const size_t C64 = (n + 63) & ~(size_t)63;
   QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, v.mp, (size_t)32,
              sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, C64, v.row);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row,
+  static const unsigned gre = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, true>, P::TPB);
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)(n < gre ? n : gre)), dim3(P::TPB), 0, st, n, v.row,
              (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
   QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
   return hipGetLastError();

@@ -95,8 +95,13 @@ __device__ __forceinline__ void kzero(KState& s) {
   for (int i = 0; i < 25; ++i) s.a[i] = {0u, 0u};
 }
 
-__device__ __forceinline__ void keccak_f(KState& s) {
-#pragma unroll 1
+// QRK_KECCAK_UNROLL: rounds per loop iteration (1, 2, 3, 4, 6 ...; 24 = fully unrolled)
+#ifndef QRK_KECCAK_UNROLL
+#define QRK_KECCAK_UNROLL 1
+#endif
+template <int U = QRK_KECCAK_UNROLL>
+__device__ __forceinline__ void keccak_fu(KState& s) {
+#pragma unroll U
   for (int r = 0; r < 24; ++r) {
     u2 C[5], R[5], B[25];
 #pragma unroll
@@ -155,6 +160,7 @@ __device__ __forceinline__ void keccak_f(KState& s) {
     s.a[0].hi ^= KRC_HI[r];
   }
 }
+__device__ __forceinline__ void keccak_f(KState& s) { keccak_fu<QRK_KECCAK_UNROLL>(s); }
 
 __device__ __forceinline__ void kxor(KState& s, int i, uint64_t w) {
   // i must be a compile-time constant after inlining

@@ -136,6 +136,18 @@ __global__ __launch_bounds__(256) void k_keccak_ref(uint64_t* out, int perms) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = x;
 }
 
+template <int U>
+__global__ __launch_bounds__(256) void k_keccak_u(uint64_t* out, int perms) {
+  qrk::KState s;
+  qrk::kzero(s);
+  s.a[0].lo = blockIdx.x * blockDim.x + threadIdx.x;
+  for (int p = 0; p < perms; ++p) qrk::keccak_fu<U>(s);
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 25; ++i) x ^= qrk::kword(s, i);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
 __global__ __launch_bounds__(256) void k_keccak_s64(uint64_t* out, int perms) {
   S64 s;
 #pragma unroll
@@ -217,10 +229,12 @@ int main() {
   int bad = 0;
   for (int i = 0; i < nchk * 25; ++i) bad += o1[i] != o2[i];
   printf(", \"s64_mismatch_words\": %d", bad);
-  for (int v = 0; v < 2; ++v) {
+  const char* vn[] = {"ref", "s64", "u2", "u3", "u4", "u6"};
+  for (int v = 0; v < 6; ++v) {
     for (int wpc : {8, 16}) {
       const int kb = cus * wpc, perms = 64;
-      auto fn = v ? k_keccak_s64 : k_keccak_ref;
+      void (*fns[])(uint64_t*, int) = {k_keccak_ref, k_keccak_s64, k_keccak_u<2>, k_keccak_u<3>, k_keccak_u<4>, k_keccak_u<6>};
+      auto fn = fns[v];
       hipLaunchKernelGGL(fn, dim3(kb), dim3(256), 0, 0, d64, 2);
       CHECK(hipDeviceSynchronize());
       float best = 1e30f;
@@ -234,8 +248,8 @@ int main() {
         best = ms < best ? ms : best;
       }
       const double p = (double)kb * 256 * perms;
-      printf(", \"keccak_%s_wg%d_perms_per_s\": %.4e, \"keccak_%s_wg%d_Tops_at_4320\": %.3f", v ? "s64" : "ref", wpc,
-             p / (best * 1e-3), v ? "s64" : "ref", wpc, p * 4320 / (best * 1e-3) / 1e12);
+      printf(", \"keccak_%s_wg%d_perms_per_s\": %.4e, \"keccak_%s_wg%d_Tops_at_4320\": %.3f", vn[v], wpc,
+             p / (best * 1e-3), vn[v], wpc, p * 4320 / (best * 1e-3) / 1e12);
     }
   }
   printf("}\n");
