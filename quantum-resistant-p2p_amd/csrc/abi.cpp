@@ -300,6 +300,12 @@ struct TimerScope {
   ~TimerScope() { g_timer = prev; }
 };
 
+// QRK_FIX_SIDE 1: on the single-stream schedule the ML-KEM SampleNTT fix-up kernel (about one
+// wave per SIMD, latency-bound) runs on the side stream beside the front hash and PRFs
+#ifndef QRK_FIX_SIDE
+#define QRK_FIX_SIDE 1
+#endif
+
 // Core batched driver over device pointers, chunked.
 static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
                      const uint8_t* i2, int32_t* status, hipStream_t st) {
@@ -342,6 +348,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   // chip and the overlap only stretches each kernel's span (profiles/r2/ab_streams*.json).
   const bool fork = ctx->streams == 2 || (ctx->streams == 0 && chunk < QRK_FORK_MAX);
   S.aux = fork ? ctx->aux : nullptr;
+  S.side = QRK_FIX_SIDE ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
   if (ctx->flag_next) {

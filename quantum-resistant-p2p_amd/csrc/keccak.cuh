@@ -97,7 +97,7 @@ __device__ __forceinline__ void kzero(KState& s) {
 
 // QRK_KECCAK_UNROLL: rounds per loop iteration (1, 2, 3, 4, 6 ...; 24 = fully unrolled)
 #ifndef QRK_KECCAK_UNROLL
-#define QRK_KECCAK_UNROLL 1
+#define QRK_KECCAK_UNROLL 2
 #endif
 template <int U = QRK_KECCAK_UNROLL>
 __device__ __forceinline__ void keccak_fu(KState& s) {

@@ -1971,18 +1971,33 @@ inline void join(const Streams& s) {
   (void)hipStreamWaitEvent(s.main, s.join, 0);
 }
 
+// fixside: run the fix-up on Streams::side (the single-stream schedule's overlap of the
+// latency-bound fix-up with the next kernels on st); the caller joins with fix_join() before
+// the core reads the sampled matrix
 template <int K>
-void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st) {
+void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st,
+                const Streams* fixside = nullptr) {
   (void)hipMemsetAsync(v.nfix, 0, 4, st);
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
              C, (uint4*)v.xof, v.fix, v.nfix);
+  hipStream_t fs = st;
+  if (fixside) {
+    (void)hipEventRecord(fixside->fork, st);
+    (void)hipStreamWaitEvent(fixside->side, fixside->fork, 0);
+    fs = fixside->side;
+  }
   // one lane per listed entry in a single pass for fix-up rates up to 1/64 (~0.7 % expected):
   // the fix-up is latency-bound (4+ sequential permutations per lane), a second grid-stride
   // pass would double it
   const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
-  QRK_LAUNCH("k_xof_fix", st, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, st, rho, stride, n, C,
+  QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C,
              (uint4*)v.xof, v.fix,
              v.nfix);
+  if (fixside) (void)hipEventRecord(fixside->join, fs);
+}
+inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }
+inline void fix_join(const Streams* fs) {
+  if (fs) (void)hipStreamWaitEvent(fs->main, fs->join, 0);
 }
 
 template <int K>
@@ -1997,11 +2012,13 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds);
+  const Streams* fs = fix_side(s);
   fork(s);
-  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd);
+  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
              n, C, 2 * K, 2 * K, v.prf);
   join(s);
+  fix_join(fs);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
              n, C, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
@@ -2019,13 +2036,15 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
     return hipGetLastError();
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
+  const Streams* fs = fix_side(s);
   fork(s);
-  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd);
+  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
   QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
              v.seeds);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
              v.seeds, n, C, 2 * K + 1, K, v.prf);
   join(s);
+  fix_join(fs);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256),
              0, st, n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
              nullptr);
@@ -2044,14 +2063,16 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
+  const Streams* fs = fix_side(s);
   fork(s);
-  launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd);
+  launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd, fs);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
   QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
              v.seeds, v.kprime, v.kbar);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
              v.seeds, n, C, 2 * K + 1, K, v.prf);
   join(s);
+  fix_join(fs);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf,
              sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
              (int32_t*)nullptr, v.kprime, v.kbar, ss);

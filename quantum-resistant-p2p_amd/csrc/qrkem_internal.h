@@ -66,6 +66,9 @@ struct Streams {
   hipStream_t main = nullptr;
   hipStream_t aux = nullptr;  // nullptr: single-stream schedule
   hipEvent_t fork = nullptr, join = nullptr;
+  // the context's side stream even on the single-stream schedule: ML-KEM runs its SampleNTT
+  // fix-up kernel there, beside the front hash (nullptr: fix-up on main)
+  hipStream_t side = nullptr;
   // single-shot completion flag (fine-grained host memory, device address): the one-launch ML-KEM
   // kernels store `ticket` there once their outputs are visible to the host
   uint32_t* done = nullptr;
