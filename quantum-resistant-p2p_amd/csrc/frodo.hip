@@ -27,6 +27,7 @@
 // k_fr_kg_rows (lane / row: Gen(A) row and B = AS + E on VALU), k_fr_kg_pack.
 #include "aes.cuh"
 #include "keccak.cuh"
+#include "keccak_coop.cuh"
 #include "qrkem_internal.h"
 
 namespace qrk {
@@ -1119,9 +1120,128 @@ __global__ __launch_bounds__(256) void k_fr_kg_pkh(const uint8_t* __restrict__ p
   for (int w = 0; w < P::SEC / 8; ++w) o[w] = kword(s, w);
 }
 
+// ---------------------------------------------------------------- small batches: wave-cooperative sponges
+// For a handful of handshakes (the reference's one-call-per-handshake pattern) the lane-per-hs
+// sponge kernels above are latency-bound: one lane runs H(pk) (58 / 94 / 129 permutations), the
+// SE stream (123 / 231 / 318) and ss = H(ct || k) in sequence at ~9 us per permutation on a wave
+// that is alone on its SIMD.  Below QRK_FR_COOP_MAX handshakes these four sponges run one state
+// per wave (keccak_coop.cuh, ~2.7 us per permutation) with identical outputs.
+#ifndef QRK_FR_COOP_MAX
+#define QRK_FR_COOP_MAX 256
+#endif
+
+// H(pk) of the hs's pk as the wave's state (coop lanes idx < SEC/8 hold pkh)
+template <int N>
+__device__ __forceinline__ CState pkh_coop(const uint8_t* __restrict__ pk_row, const Coop& c) {
+  using P = FP<N>;
+  const uint64_t* pkw = (const uint64_t*)pk_row;
+  CState s;
+  coop_absorb<P::RW, P::PK / 8, DS_SHAKE>(s, c, [&](int w) { return pkw[w]; });
+  return s;
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_fr_front_enc_c(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ mu,
+                                                       size_t n, uint64_t* __restrict__ seeds) {
+  using P = FP<N>;
+  constexpr int PW = P::SEC / 8, GW = (P::SEC + P::MU) / 8;
+  static_assert((P::SEC + P::MU) % 8 == 0 && GW < P::RW, "pkh || mu is whole words of one block");
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const bool canon = coop_canon(c);
+  const CState h = pkh_coop<N>(pk + hs * P::PK, c);
+  const uint64_t* muw = (const uint64_t*)(mu + hs * P::MU);
+  uint64_t* sd = seeds + hs * 16;
+  CState g;  // (seedSE || k) = H(pkh || mu): each pkh word stays on its lane
+  if (i >= 0 && i < PW) {
+    cs_xor(g, cs_word(h));
+    if (canon) sd[8 + i] = cs_word(h);
+  }
+  if (i >= PW && i < GW) cs_xor(g, muw[i - PW]);
+  if (i == GW) g.lo ^= DS_SHAKE;
+  if (i == P::RW - 1) g.hi ^= 0x80000000u;
+  g = kf_coop(g, c);
+  if (canon && i < 2 * PW) sd[i] = cs_word(g);
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_fr_se_stream_c(const uint64_t* __restrict__ seeds, size_t n, int domain, int W,
+                                                       int RAWW, uint64_t* __restrict__ raw) {
+  using P = FP<N>;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const bool canon = coop_canon(c);
+  const uint64_t* sd = seeds + hs * 16;
+  // word i of domain || seedSE: the seed shifted up by one byte
+  CState s;
+  if (i >= 0 && i < 5) {
+    const uint64_t cur = i < P::SEC / 8 ? sd[i] : 0;
+    const uint64_t prv = i == 0 ? (uint64_t)domain : (i - 1 < P::SEC / 8 ? sd[i - 1] >> 56 : 0);
+    cs_xor(s, prv | (cur << 8));
+  }
+  if (i == (1 + P::SEC) / 8) cs_xor(s, (uint64_t)DS_SHAKE << (8 * ((1 + P::SEC) % 8)));
+  if (i == P::RW - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+  coop_squeeze<P::RW>(s, c, W, [&](int w, uint64_t v) {
+    if (canon) raw[tidx(hs, w, RAWW)] = v;
+  });
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_fr_ss_c(const uint8_t* __restrict__ ct, size_t n,
+                                                const uint64_t* __restrict__ kk, uint8_t* __restrict__ ss) {
+  using P = FP<N>;
+  constexpr int CW = P::CT / 8;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  const uint64_t* cw = (const uint64_t*)(ct + hs * P::CT);
+  const uint64_t* kw = kk + hs * 4;
+  CState s;
+  coop_absorb<P::RW, CW + P::SEC / 8, DS_SHAKE>(s, c, [&](int w) { return w < CW ? cw[w] : kw[w - CW]; });
+  if (coop_canon(c) && c.idx < P::SEC / 8) ((uint64_t*)(ss + hs * P::SEC))[c.idx] = cs_word(s);
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_fr_kg_pkh_c(const uint8_t* __restrict__ pk, size_t n, uint8_t* __restrict__ sk) {
+  using P = FP<N>;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  const CState h = pkh_coop<N>(pk + hs * P::PK, c);
+  uint64_t* o = (uint64_t*)(sk + hs * P::SK + P::SEC + P::PK + 2 * N * NBAR);
+  if (coop_canon(c) && c.idx < P::SEC / 8) o[c.idx] = cs_word(h);
+}
+
 // ---------------------------------------------------------------- launchers
 inline unsigned blocks_for(size_t t, int per = 256) { return (unsigned)((t + per - 1) / per); }
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
+
+inline bool coop_path(size_t n) { return n <= QRK_FR_COOP_MAX; }
+
+// SHAKE(domain || seedSE) sampler stream of W words per handshake
+template <int N>
+void launch_se(const View<N>& v, size_t n, int domain, int W, hipStream_t st) {
+  if (coop_path(n))
+    QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream_c<N>, dim3((unsigned)n), dim3(64), 0, st, v.seeds, n, domain, W, W,
+               v.raw);
+  else
+    QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream<N>, dim3(blocks_for(n)), dim3(256), 0, st, v.seeds, n, domain, W,
+               W, v.raw);
+}
+
+// ss = H(ct || kk)
+template <int N>
+void launch_ss(const uint8_t* ct, size_t n, const View<N>& v, uint8_t* ss, hipStream_t st) {
+  if (coop_path(n))
+    QRK_LAUNCH("k_fr_ss", st, k_fr_ss_c<N>, dim3((unsigned)n), dim3(64), 0, st, ct, n, v.kk, ss);
+  else
+    QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
+}
 
 // per-wave partial sums of S'A for every handshake of the chunk (Gen(A) fused)
 template <int N, bool AES>
@@ -1144,15 +1264,18 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   using P = FP<N>;
   const size_t C = round64(n);
   View<N> v = carve<N>(scratch, C);
-  QRK_LAUNCH("k_fr_front_enc", st, k_fr_front_enc<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, mu, n, v.seeds);
-  QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream<N>, dim3(blocks_for(n)), dim3(256), 0, st, v.seeds, n, 0x96,
-             P::SE_WORDS, P::SE_WORDS, v.raw);
+  if (coop_path(n)) {
+    QRK_LAUNCH("k_fr_front_enc", st, k_fr_front_enc_c<N>, dim3((unsigned)n), dim3(64), 0, st, pk, mu, n, v.seeds);
+  } else {
+    QRK_LAUNCH("k_fr_front_enc", st, k_fr_front_enc<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, mu, n, v.seeds);
+  }
+  launch_se<N>(v, n, 0x96, P::SE_WORDS, st);
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk, P::PK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
              v.ep16, v.epp16, v.part, v.seeds, mu, (size_t)P::MU, ct, nullptr, nullptr, (size_t)0, v.kk);
-  QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
+  launch_ss<N>(ct, n, v, ss, st);
   return hipGetLastError();
 }
 
@@ -1164,15 +1287,14 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   const uint8_t* pk_in_sk = sk + P::SEC;
   QRK_LAUNCH("k_fr_dec_m", st, k_fr_dec_m<N>, dim3((unsigned)n), dim3(256), 0, st, n, ct, sk, v.seeds);
   QRK_LAUNCH("k_fr_g2_dec", st, k_fr_g2_dec<N>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.seeds);
-  QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream<N>, dim3(blocks_for(n)), dim3(256), 0, st, v.seeds, n, 0x96,
-             P::SE_WORDS, P::SE_WORDS, v.raw);
+  launch_se<N>(v, n, 0x96, P::SE_WORDS, st);
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk_in_sk, P::SK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
              v.sp8, v.ep16, v.epp16, v.part, v.seeds, (const uint8_t*)(v.seeds + 12), (size_t)128, nullptr, ct, sk,
              (size_t)P::SK, v.kk);
-  QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
+  launch_ss<N>(ct, n, v, ss, st);
   return hipGetLastError();
 }
 
@@ -1183,8 +1305,7 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   View<N> v = carve<N>(scratch, C);
   QRK_LAUNCH("k_fr_kg_front", st, k_fr_kg_front<N>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds);
-  QRK_LAUNCH("k_fr_se_stream", st, k_fr_se_stream<N>, dim3(blocks_for(n)), dim3(256), 0, st, v.seeds, n, 0x5F,
-             P::KG_WORDS, P::KG_WORDS, v.raw);
+  launch_se<N>(v, n, 0x5F, P::KG_WORDS, st);
   // S^T -> sp8 ([8][NP] int8), E -> ep16 as [N][8]
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
@@ -1204,7 +1325,10 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
                spair, v.ep16, v.part);
   }
   QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(256), 0, st, n, v.part, v.sp8, pk, sk);
-  QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, n, sk);
+  if (coop_path(n))
+    QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh_c<N>, dim3((unsigned)n), dim3(64), 0, st, pk, n, sk);
+  else
+    QRK_LAUNCH("k_fr_kg_pkh", st, k_fr_kg_pkh<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, n, sk);
   return hipGetLastError();
 }
 

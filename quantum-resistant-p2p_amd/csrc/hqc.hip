@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "keccak.cuh"
+#include "keccak_coop.cuh"
 #include "qrkem_internal.h"
 
 namespace qrk {
@@ -316,6 +317,121 @@ __global__ __launch_bounds__(256) void k_hqc_hash(const uint64_t* __restrict__ m
   uint64_t* o = (uint64_t*)(ss + hs * SSB);
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = kword(s, i);
+}
+
+// ---------------------------------------------------------------- small batches: wave-cooperative sponges
+// Below QRK_HQC_COOP_MAX handshakes the seedexpander streams and the K hash run one sponge state
+// per wave (keccak_coop.cuh, ~2.7 us per permutation against ~9 us for a lane alone on its SIMD):
+// the reference calls one handshake at a time, where the hash's 33 / 67 / 106 sequential
+// permutations and the h stream are the critical path.  Same outputs as the lane kernels above.
+#ifndef QRK_HQC_COOP_MAX
+#define QRK_HQC_COOP_MAX 256
+#endif
+
+// seedexpander(seed) = SHAKE256(seed || 0x02) with the 40-byte seed at any alignment
+__device__ __forceinline__ CState seedexp_coop(const uint8_t* __restrict__ seed, const Coop& c) {
+  const int i = c.idx;
+  CState s;
+  if (i >= 0 && i < 5) cs_xor(s, ld64u(seed + 8 * i));
+  if (i == 5) cs_xor(s, 0x02ull | (0x1Full << 8));
+  if (i == RW_SHAKE256 - 1) s.hi ^= 0x80000000u;
+  return kf_coop(s, c);
+}
+__device__ __forceinline__ void squeeze_coop(CState& s, const Coop& c, uint64_t* out, int NW) {
+  const bool canon = coop_canon(c);
+  coop_squeeze<RW_SHAKE256>(s, c, NW, [&](int w, uint64_t v) {
+    if (canon) out[w] = v;
+  });
+}
+
+// wave b < n: x, y of hs b; wave n + b: the h stream of hs b
+template <int L>
+__global__ __launch_bounds__(64) void k_hqc_kg_expand_c(const uint8_t* __restrict__ coins, size_t n,
+                                                        uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  const size_t inst = blockIdx.x, hs = inst % n;
+  const bool hstream = inst >= n;
+  const Coop c = coop_init();
+  const uint8_t* cb = coins + hs * P::KPC;
+  uint64_t* r = row + hs * P::ROWW;
+  CState s = seedexp_coop(hstream ? cb + SEED + P::K : cb, c);
+  if (hstream)
+    squeeze_coop(s, c, r + 2 * P::RWW, P::NHW);
+  else
+    squeeze_coop(s, c, r, 2 * P::RWW);
+}
+
+// wave b < n: theta = G(m || pk[0:80] || salt), then SE(theta) -> r1, r2, e of hs b;
+// wave n + b: SE(pk_seed) -> h of hs b
+template <int L>
+__global__ __launch_bounds__(64) void k_hqc_enc_expand_c(const uint8_t* __restrict__ m, size_t m_stride,
+                                                         const uint8_t* __restrict__ pk, size_t pk_stride,
+                                                         const uint8_t* __restrict__ salt, size_t salt_stride,
+                                                         size_t n, uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  constexpr int KW = P::K / 8, TW = KW + 10 + 2 + 1;  // m || pk[0:80] || salt || (0x03, 0x1F)
+  static_assert(TW <= RW_SHAKE256, "one block");
+  const size_t inst = blockIdx.x, hs = inst % n;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const uint8_t* pp = pk + hs * pk_stride;
+  uint64_t* r = row + hs * P::ROWW;
+  if (inst >= n) {
+    CState s = seedexp_coop(pp, c);
+    squeeze_coop(s, c, r + 2 * P::RWR + P::RWE, P::NHW);
+    return;
+  }
+  const uint8_t* mp = m + hs * m_stride;
+  const uint8_t* sp = salt + hs * salt_stride;
+  CState g;
+  if (i >= 0 && i < KW) cs_xor(g, ld64u(mp + 8 * i));
+  if (i >= KW && i < KW + 10) cs_xor(g, ld64u(pp + 8 * (i - KW)));
+  if (i >= KW + 10 && i < KW + 12) cs_xor(g, ld64u(sp + 8 * (i - KW - 10)));
+  if (i == KW + 12) cs_xor(g, 0x03ull | (0x1Full << 8));
+  if (i == RW_SHAKE256 - 1) g.hi ^= 0x80000000u;
+  g = kf_coop(g, c);
+  // seedexpander(theta[0:40]): every theta word stays on its lane
+  CState s;
+  if (i >= 0 && i < 5) cs_xor(s, cs_word(g));
+  if (i == 5) cs_xor(s, 0x02ull | (0x1Full << 8));
+  if (i == RW_SHAKE256 - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+  squeeze_coop(s, c, r, 2 * P::RWR + P::RWE);
+}
+
+template <int L>
+__global__ __launch_bounds__(64) void k_hqc_dec_expand_c(const uint8_t* __restrict__ sk, size_t n,
+                                                         uint64_t* __restrict__ row) {
+  using P = HQ<L>;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  CState s = seedexp_coop(sk + hs * P::SK, c);
+  squeeze_coop(s, c, row + hs * P::ROWW, 2 * P::RWW);
+}
+
+template <int L>
+__global__ __launch_bounds__(64) void k_hqc_hash_c(const uint64_t* __restrict__ msg, size_t n, uint8_t* __restrict__ ss) {
+  using P = HQ<L>;
+  constexpr int RW = RW_SHAKE256, NFULL = (P::MW - 1) / RW, REM = P::MW - NFULL * RW;
+  const size_t hs = blockIdx.x;
+  if (hs >= n) return;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  const bool rl = i >= 0 && i < RW;
+  const uint64_t* m = msg + hs * P::MW;
+  CState s;
+  uint64_t nxt = (rl && (NFULL > 0 || i < REM)) ? m[i] : 0;
+#pragma unroll 1
+  for (int b = 0; b < NFULL; ++b) {
+    cs_xor(s, nxt);
+    nxt = (rl && (b + 1 < NFULL || i < REM)) ? m[(b + 1) * RW + i] : 0;
+    s = kf_coop(s, c);
+  }
+  cs_xor(s, nxt);
+  if (i == RW - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+  if (coop_canon(c) && i < 8) ((uint64_t*)(ss + hs * SSB))[i] = cs_word(s);
 }
 
 // ---------------------------------------------------------------- workgroup / hs helpers
@@ -1179,6 +1295,26 @@ unsigned wg_grid(size_t n, Kern kern, int tpb) {
 }
 
 template <int L>
+void launch_enc_expand(const uint8_t* m, size_t m_stride, const uint8_t* pk, size_t pk_stride, const uint8_t* salt,
+                       size_t salt_stride, size_t n, uint64_t* row, hipStream_t st) {
+  if (n <= QRK_HQC_COOP_MAX) {
+    QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand_c<L>, dim3((unsigned)(2 * n)), dim3(64), 0, st, m, m_stride, pk,
+               pk_stride, salt, salt_stride, n, row);
+  } else {
+    const size_t C64 = (n + 63) & ~(size_t)63;
+    QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, m, m_stride,
+               pk, pk_stride, salt, salt_stride, n, C64, row);
+  }
+}
+template <int L>
+void launch_hash(const uint64_t* msg, size_t n, uint8_t* ss, hipStream_t st) {
+  if (n <= QRK_HQC_COOP_MAX)
+    QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash_c<L>, dim3((unsigned)n), dim3(64), 0, st, msg, n, ss);
+  else
+    QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, msg, n, ss);
+}
+
+template <int L>
 size_t scratch_t(size_t C) {
   using P = HQ<L>;
   return al256(C * P::ROWW * 8) + al256(C * P::MW * 8) + al256(C * 32) + al256(C * 4);
@@ -1207,7 +1343,10 @@ View carve(void* base, size_t C) {
 template <int L>
 hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, hipStream_t st) {
   View v = carve<L>(scratch, n);
-  QRK_LAUNCH("k_hqc_kg_expand", st, k_hqc_kg_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, v.row);
+  if (n <= QRK_HQC_COOP_MAX)
+    QRK_LAUNCH("k_hqc_kg_expand", st, k_hqc_kg_expand_c<L>, dim3((unsigned)(2 * n)), dim3(64), 0, st, coins, n, v.row);
+  else
+    QRK_LAUNCH("k_hqc_kg_expand", st, k_hqc_kg_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, v.row);
   QRK_LAUNCH("k_hqc_kg_mul", st, k_hqc_kg_mul<L>, dim3((unsigned)n), dim3(HQ<L>::TPB), 0, st, n, v.row, coins, pk, sk);
   return hipGetLastError();
 }
@@ -1217,14 +1356,12 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
                     hipStream_t st) {
   using P = HQ<L>;
   View v = carve<L>(scratch, n);
-  const size_t C64 = (n + 63) & ~(size_t)63;
-  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, coins,
-             (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, C64, v.row);
+  launch_enc_expand<L>(coins, (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, v.row, st);
   static const unsigned genc = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, false>, P::TPB);
   QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)(n < genc ? n : genc)), dim3(P::TPB), 0, st, n, v.row, coins,
              pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
              v.msg);
-  QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
+  launch_hash<L>(v.msg, n, ss, st);
   return hipGetLastError();
 }
 
@@ -1234,20 +1371,22 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   using P = HQ<L>;
   View v = carve<L>(scratch, n);
   int32_t* stp = status ? status : v.st;
-  QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.row);
+  if (n <= QRK_HQC_COOP_MAX)
+    QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand_c<L>, dim3((unsigned)n), dim3(64), 0, st, sk, n, v.row);
+  else
+    QRK_LAUNCH("k_hqc_dec_expand", st, k_hqc_dec_expand<L>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.row);
   // the RM stage's symbols go through the K-hash message area, which is free until the re-encryption
   uint8_t* syms = (uint8_t*)v.msg;
   QRK_LAUNCH("k_hqc_decode", st, k_hqc_decode<L>, dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, ct, syms,
              (size_t)P::MW * 8);
   QRK_LAUNCH("k_hqc_rs", st, k_hqc_rs<L>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, n, (const uint8_t*)syms,
              (size_t)P::MW * 8, v.mp);
-  const size_t C64 = (n + 63) & ~(size_t)63;
-  QRK_LAUNCH("k_hqc_enc_expand", st, k_hqc_enc_expand<L>, dim3(blocks_for(2 * C64)), dim3(256), 0, st, v.mp, (size_t)32,
-             sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, C64, v.row);
+  launch_enc_expand<L>(v.mp, (size_t)32, sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row,
+                       st);
   static const unsigned gre = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, true>, P::TPB);
   QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)(n < gre ? n : gre)), dim3(P::TPB), 0, st, n, v.row,
              (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
-  QRK_LAUNCH("k_hqc_hash", st, k_hqc_hash<L>, dim3(blocks_for(n)), dim3(256), 0, st, v.msg, n, ss);
+  launch_hash<L>(v.msg, n, ss, st);
   return hipGetLastError();
 }
 

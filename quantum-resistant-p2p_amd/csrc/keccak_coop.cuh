@@ -203,4 +203,76 @@ __device__ __forceinline__ void keccak_f_coop(uint32_t& lo, uint32_t& hi, const 
   }
 }
 
+// One sponge state spread over the wave: this lane's 64-bit word (index Coop::idx).
+struct CState {
+  uint32_t lo = 0, hi = 0;
+};
+__device__ __forceinline__ void cs_xor(CState& s, uint64_t w) {
+  s.lo ^= (uint32_t)w;
+  s.hi ^= (uint32_t)(w >> 32);
+}
+__device__ __forceinline__ uint64_t cs_word(const CState& s) { return ((uint64_t)s.hi << 32) | s.lo; }
+// word w (per lane) of the state, fetched from the lane that holds it
+__device__ __forceinline__ uint64_t cs_get(const CState& s, int w) {
+  const int a = 4 * coop_lane_of(w);
+  return ((uint64_t)bperm(a, s.hi) << 32) | bperm(a, s.lo);
+}
+// the permutation as a call (one copy of the unrolled rounds per kernel, not one per call site);
+// QRK_COOP_CALL=0 inlines it at every call site
+#ifndef QRK_COOP_CALL
+#define QRK_COOP_CALL 1
+#endif
+#if QRK_COOP_CALL
+static __device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+CState kf_coop(CState s, Coop c) {
+  keccak_f_coop(s.lo, s.hi, c);
+  return s;
+}
+
+// Sponge absorb of NW message words ld(0..NW-1) at rate RW, padded with domain byte DS; the
+// lanes holding state words 0..RW-1 each load their word of the next block before the current
+// block's permutation.
+template <int RW, int NW, uint32_t DS, typename Loader>
+__device__ __forceinline__ void coop_absorb(CState& s, const Coop& c, Loader ld) {
+  constexpr int NFULL = NW / RW, TAIL = NW % RW;
+  const int i = c.idx;
+  const bool rl = i >= 0 && i < RW;
+  uint64_t nxt = (rl && (NFULL > 0 || i < TAIL)) ? ld(i) : 0;
+#pragma unroll 1
+  for (int b = 0; b < NFULL; ++b) {
+    cs_xor(s, nxt);
+    nxt = (rl && (b + 1 < NFULL || i < TAIL)) ? ld((b + 1) * RW + i) : 0;
+    s = kf_coop(s, c);
+  }
+  cs_xor(s, nxt);
+  if (i == TAIL) s.lo ^= DS;
+  if (i == RW - 1) s.hi ^= 0x80000000u;
+  s = kf_coop(s, c);
+}
+
+
+// the lane that owns state word c.idx (replica lanes mirror it and must not write outputs twice)
+__device__ __forceinline__ bool coop_canon(const Coop& c) {
+  return c.idx >= 0 && (int)(threadIdx.x & 63) == coop_lane_of(c.idx);
+}
+
+// Squeeze NW words of an absorbed sponge: word w goes to out(w, value) on the lane that holds
+// it (lanes idx < RW of each block), permuting between blocks.
+template <int RW, typename Store>
+__device__ __forceinline__ void coop_squeeze(CState& s, const Coop& c, int NW, Store out) {
+  const int i = c.idx;
+  const bool rl = i >= 0 && i < RW;
+  int w = 0;
+#pragma unroll 1
+  while (true) {
+    if (rl && w + i < NW) out(w + i, cs_word(s));
+    w += RW;
+    if (w >= NW) break;
+    s = kf_coop(s, c);
+  }
+}
+
 }  // namespace qrk
