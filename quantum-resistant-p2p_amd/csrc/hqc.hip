@@ -468,6 +468,15 @@ __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, 
 // The first term: every s_j broadcast once (v_readlane) and compared with all lanes (a ballot per
 // register, masked to j > i, OR-ed into 64-bit lane masks); the chain: pointer jumping over
 // (replaced, next) words gathered with ds_bpermute, ceil(log2 w) rounds.
+// QRK_HQC_DEDUPE_ROT 1: the first term by lane rotations (63 rounds of ds_bpermute, no SGPR
+// round trips); 2: v_readlane broadcasts into per-lane VGPR accumulators (no ballots / SALU);
+// 0 (default): one v_readlane broadcast of s_j per j, ballot per register.  Variant 2 is also
+// slower (HQC-128 enc_mul 0.85 vs 0.77 ms, profiles/r2/ab_hqc_dedupe_vreg_rejected.jsonl).  A/B on one box
+// (profiles/r2/ab_hqc_dedupe_rot_rejected.jsonl): the rotations are slower (HQC-128 enc_mul 0.976
+// vs 0.766 ms) -- the permutes compete with the products for the CU's LDS.
+#ifndef QRK_HQC_DEDUPE_ROT
+#define QRK_HQC_DEDUPE_ROT 0
+#endif
 template <int WT>
 __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
   constexpr int NE = (WT + 63) / 64;
@@ -478,6 +487,74 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
   uint32_t v[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
+#if QRK_HQC_DEDUPE_ROT == 1
+  // first term, all lanes at once: element (e, l) meets element (f, (l + d) mod 64) for every
+  // rotation d (one ds_bpermute per register and d, independent across d, no SGPR round trips);
+  // index 64 f + l' exceeds 64 e + l iff f > e, or f == e and l + d < 64 (no wrap).  Padding
+  // lanes hold 0xFFFFFFFF, never equal to a support (< n).
+  bool hit[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    hit[e] = false;
+#pragma unroll
+    for (int f = e + 1; f < NE; ++f) hit[e] = hit[e] || v[f] == v[e];  // d = 0
+  }
+  // rotations in batches of DB: every permute of a batch is issued before the first compare,
+  // so the LDS round trips overlap instead of costing one each
+  constexpr int DB = 8;
+#pragma unroll
+  for (int d0 = 1; d0 < 64; d0 += DB) {
+    uint32_t p[DB][NE];
+#pragma unroll
+    for (int k = 0; k < DB; ++k)
+#pragma unroll
+      for (int f = 0; f < NE; ++f)
+        if (d0 + k < 64) p[k][f] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * ((lane + d0 + k) & 63), (int)v[f]);
+    __builtin_amdgcn_sched_barrier(0);  // keep the batch's permutes ahead of its compares
+#pragma unroll
+    for (int k = 0; k < DB; ++k) {
+      if (d0 + k >= 64) continue;
+      const bool nowrap = lane < 64 - (d0 + k);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        bool h = nowrap && p[k][e] == v[e];
+#pragma unroll
+        for (int f = e + 1; f < NE; ++f) h = h || p[k][f] == v[e];
+        hit[e] = hit[e] || h;
+      }
+    }
+  }
+  uint32_t x[NE];  // REP | next chain index (or NONE)
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const uint32_t i = 64 * e + lane;
+    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
+    x[e] = (hit[e] ? REP : 0u) | ptr;
+  }
+#elif QRK_HQC_DEDUPE_ROT == 2
+  // first term with per-lane accumulators in VGPRs: s_j broadcast by v_readlane, then
+  // hit |= ((v ^ s_j) - 1) & (lane - lim) -- bit 31 set iff v == s_j (both < 2^15) and i < j --
+  // four full-rate VALU ops per (j, register), no ballots and no SALU round trips
+  uint32_t hacc[NE] = {};
+#pragma unroll
+  for (int j = 1; j < WT; ++j) {
+    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      if (64 * e >= j) continue;  // no i < j in this register
+      const int lim = j - 64 * e;  // lanes below lim have i < j
+      const uint32_t eq = (v[e] ^ sj) - 1u;
+      hacc[e] |= lim >= 64 ? eq : (eq & (uint32_t)(lane - lim));
+    }
+  }
+  uint32_t x[NE];  // REP | next chain index (or NONE)
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const uint32_t i = 64 * e + lane;
+    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
+    x[e] = (hacc[e] & 0x80000000u) | ptr;  // REP is bit 31
+  }
+#else
   uint64_t dup[NE] = {};
 #pragma unroll
   for (int j = 1; j < WT; ++j) {
@@ -497,6 +574,7 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
     const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
     x[e] = ((dup[e] >> lane) & 1 ? REP : 0u) | ptr;
   }
+#endif
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
     uint32_t y[NE];
@@ -604,6 +682,12 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   }
 }
 
+// QRK_HQC_DPP_WIN 1: each window's last word from the neighbouring lane by DPP wave_shl:1 (one LDS
+// read fewer per window); A/B slower (HQC-128 enc_mul 0.818 vs 0.766 ms, HQC-256 6.18 vs 4.98 ms,
+// profiles/r2/ab_hqc_dpp_win_rejected.jsonl), off by default
+#ifndef QRK_HQC_DPP_WIN
+#define QRK_HQC_DPP_WIN 0
+#endif
 // acc[c] ^= word (j0 + c) of X^k D-operand for the positions k of sup in this thread's class
 // (partial sums; prod_combine adds the classes)
 template <int L, int NV, int WPT, int NBT>
@@ -613,6 +697,7 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
   constexpr int PC = P::TPB / NBT;
   const int tt = hq_tid();
   const int j0 = (tt % NBT) * WPT;
+  const bool lane63 = (tt & 63) == 63;
   // one operand: unrolled so the next position's support read and window are in flight together;
   // two operands: not unrolled (both windows already in flight; keeps <= 64 VGPRs, 8 waves / SIMD)
   constexpr int UNR = NV == 1 ? 2 : 1;
@@ -625,8 +710,18 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       uint32_t w[WPT + 1];
+#if QRK_HQC_DPP_WIN
+      // the window's last word is the next lane's first (a wave's lanes own consecutive
+      // windows at the same position): DPP wave_shl:1, one LDS read fewer per window; lane 63's
+      // neighbour is in the next wave, it reads its own
+#pragma unroll
+      for (int c = 0; c < WPT; ++c) w[c] = D[v][off + c];
+      w[WPT] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[0], 0x130, 0xF, 0xF, false);
+      if (lane63) w[WPT] = D[v][off + WPT];
+#else
 #pragma unroll
       for (int c = 0; c <= WPT; ++c) w[c] = D[v][off + c];
+#endif
 #pragma unroll
       for (int c = 0; c < WPT; ++c) acc[v][c] ^= alignbit(w[c + 1], w[c], sh);
     }

@@ -6,7 +6,9 @@
 //   rho/pi  : 48 v_alignbit/v_perm (funnel-shift rotates; pi is register renaming)
 //   chi     : 50 v_bitop3 (a ^ (~b & c), selected by the compiler)
 //   iota    : 2 v_xor
-// = 180 VALU instructions per round, 4320 per permutation, no moves.
+// = 180 VALU instructions per round, 4320 per permutation, no moves; 58 of them (the rotations)
+// issue at half rate on gfx950, and so do the 64-bit shifts that could replace them
+// (tools/rot64_probe.hip).  Two rounds per loop iteration (QRK_KECCAK_UNROLL).
 // XOR3 is emitted through inline asm because hipcc (ROCm 7.2) splits
 // __builtin_amdgcn_bitop3_b32(...,0x96) back into two v_xor_b32.
 //
