@@ -141,3 +141,27 @@ def test_multichunk_640(engines, alg):
     oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec_h), 8)
     assert np.array_equal(pk_h, opk) and np.array_equal(sk_h, osk)
     assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
+
+
+@pytest.mark.parametrize("alg", ["FrodoKEM-640-SHAKE", "FrodoKEM-640-AES", "FrodoKEM-976-SHAKE"])
+@pytest.mark.parametrize("n", [256, 257])
+def test_coop_lane_boundary(engines, alg, n):
+    """n = 256 runs H(pk), the SE stream and ss = H(ct || k) on the wave-cooperative sponges
+    (QRK_FR_COOP_MAX), n = 257 on the lane-per-handshake kernels: both byte-exact vs the oracle,
+    including tampered-ciphertext Decaps (implicit rejection through H(ct' || s))."""
+    import oracle as orc
+    eng = engines[alg]
+    kc, ec = _coins(alg, n, 4000 + n)
+    pk, sk = eng.keypair(coins=_dev(kc))
+    ct, ss = eng.encaps(pk, coins=_dev(ec))
+    ct_h = _host(ct)
+    bad = ct_h.copy()
+    bad[1::2, 7] ^= 0x10
+    ss2 = eng.decaps(sk, ct)
+    ss3 = eng.decaps(sk, _dev(bad))
+    pk, sk, ss, ss2, ss3 = map(_host, (pk, sk, ss, ss2, ss3))
+    opk, osk = orc.batch_keypair(alg, kc, 8)
+    assert np.array_equal(pk, opk) and np.array_equal(sk, osk)
+    oct_, oss = orc.batch_encaps(alg, opk, ec, 8)
+    assert np.array_equal(ct_h, oct_) and np.array_equal(ss, oss) and np.array_equal(ss2, oss)
+    assert np.array_equal(ss3, orc.batch_decaps(alg, osk, bad, 8))

@@ -201,3 +201,28 @@ def test_supports_duplicate_removal(engines, alg):
         got = _host(engines[alg].hqc_supports(_dev(r.view(np.int32)), kind)).view(np.uint32)
         for s, g in zip(sups, got):
             assert list(g) == H.remove_duplicates(s)
+
+
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("n", [256, 257])
+def test_coop_lane_boundary(engines, alg, n):
+    """n = 256 runs the seedexpanders and the K hash on the wave-cooperative sponges
+    (QRK_HQC_COOP_MAX), n = 257 on the lane kernels: byte-exact vs the oracle, tampered
+    ciphertexts with the oracle's status."""
+    import oracle as orc
+    eng = engines[alg]
+    kc, ec = _coins(alg, n, 6000 + n)
+    pk, sk = eng.keypair(coins=_dev(kc))
+    ct, ss = eng.encaps(pk, coins=_dev(ec))
+    ct_h = _host(ct)
+    bad = ct_h.copy()
+    bad[1::2, 11] ^= 0x04
+    ss2 = eng.decaps(sk, ct)
+    ss3, st3 = eng.decaps(sk, _dev(bad), return_status=True)
+    pk, sk, ss, ss2, ss3, st3 = map(_host, (pk, sk, ss, ss2, ss3, st3))
+    opk, osk = orc.batch_keypair(alg, kc)
+    assert np.array_equal(pk, opk) and np.array_equal(sk, osk)
+    oct_, oss = orc.batch_encaps(alg, opk, ec)
+    assert np.array_equal(ct_h, oct_) and np.array_equal(ss, oss) and np.array_equal(ss2, oss)
+    ref_ss, ref_st = orc.batch_decaps(alg, osk, bad, with_status=True)
+    assert np.array_equal(ss3, ref_ss) and np.array_equal(st3, ref_st)
