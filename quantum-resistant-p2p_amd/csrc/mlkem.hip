@@ -236,6 +236,9 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #ifndef QRK_XOF_CMP
 #define QRK_XOF_CMP 1
 #endif
+#ifndef QRK_XOF_TIMING_ONLY
+#define QRK_XOF_TIMING_ONLY 0
+#endif
 // QRK_XOF_ACC 1: SampleNTT acceptance as a shifted difference (compact_block below); A/B on one
 // box no faster than v_cmp + v_cndmask (profiles/r2/ab_xof_acc_rejected.jsonl), kept as an option
 #ifndef QRK_XOF_ACC
@@ -266,6 +269,27 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 // `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
 // 8-11 are zero, so an entry address is one v_bitop3_b32, (pos & 0xF00) | rb, with the static
 // LDS base folded into the ds_write offset.
+// QRK_XOF_PIPE 1: a completed chunk's 8 ring entries are read when it completes and packed +
+// stored one triplet later (or after the block), so the LDS read latency is not waited for
+// on the spot
+#ifndef QRK_XOF_PIPE
+#define QRK_XOF_PIPE 1
+#endif
+struct XofPend {
+  uint32_t r[8];  // the chunk's ring entries, in order
+  int ch = -1;    // its chunk index, -1: nothing pending
+};
+template <int TW = 64>
+__device__ __forceinline__ void xof_pend_store(XofPend& pd, uint4* dst) {
+  if (pd.ch >= 0) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = lshl_or(pd.r[2 * j + 1], 16, pd.r[2 * j]);
+    dst[pd.ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
+    pd.ch = -1;
+  }
+}
+
 #if QRK_XOF_ACC
 // Ring layout with a 512-B entry stride: the two waves of a pair interleave their 256-B entry
 // rows (wave & 1 selects the half), so the ring is still 16 KB per 4-wave workgroup.  The
@@ -274,7 +298,8 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 // v_cmp + v_cndmask pair (about three issue slots, profiles/r1/valu_peak_r1b.json) -- and
 // P >> 9 = cnt for every cnt <= 511, so bits 9-12 of P index the ring entry directly.
 template <int TW = 64>
-__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst,
+                                              XofPend&) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
   uint32_t P = 511u * (uint32_t)(cnt + 1);
 #pragma unroll
@@ -307,8 +332,12 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 }
 #else
 template <int TW = 64>
-__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst) {
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst,
+                                              XofPend& pd) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
+#if QRK_XOF_TIMING_ONLY >= 2
+  uint32_t tsink = 0;
+#endif
 #pragma unroll
   for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
     uint32_t d[3];
@@ -325,7 +354,11 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     int pos = cnt << 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
+#if QRK_XOF_TIMING_ONLY == 3
+      tsink ^= and_or3(pos, 0xF00u, rb) + (uint32_t)c[e];  // timing probe: no LDS write
+#else
       *(uint32_t*)(ring_all + and_or3(pos, 0xF00u, rb)) = (uint32_t)c[e];
+#endif
 #if QRK_XOF_CMP
       pos += c[e] < Q ? 256 : 0;
 #else
@@ -337,14 +370,34 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     }
     cnt = pos >> 8;
     const int ch = before >> 3;
+#if QRK_XOF_PIPE
+    // the chunk completed one triplet ago: its ring reads were issued then, so they have
+    // landed by now (a wave's LDS instructions execute in issue order, so the reads saw the
+    // chunk before this triplet's writes could reuse its slots)
+    xof_pend_store<TW>(pd, dst);
     if ((cnt >> 3) != ch && ch < 32) {
+      const uint32_t* r = ring + (ch & 1) * 8 * 64;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pd.r[j] = r[j * 64];
+      pd.ch = ch;
+    }
+#else
+#if QRK_XOF_TIMING_ONLY >= 2
+    if (false) {  // timing probe: no flush
+#else
+    if ((cnt >> 3) != ch && ch < 32) {
+#endif
       const uint32_t* r = ring + (ch & 1) * 8 * 64;
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 64], 16, r[(2 * j) * 64]);
       dst[ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
     }
+#endif
   }
+#if QRK_XOF_TIMING_ONLY >= 2
+  if (tsink == 0x12345678u) dst[0] = make_uint4(tsink, tsink, tsink, tsink);
+#endif
 }
 
 #endif
@@ -368,11 +421,23 @@ __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int x
   s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
   s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
   int cnt = 0;
+  XofPend pd;
 #pragma unroll 1
   for (int b = 0; b < (ALL ? MAX_XOF_BLOCKS : 3) && (!ALL || cnt < 256); ++b) {
     keccak_f(s);
-    compact_block<TW>(s, ring_all, rb, cnt, dst);
+#if QRK_XOF_TIMING_ONLY == 1
+    // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
+    // alone, the state folded into one store per block -- wrong output, never a default build
+    uint32_t f = 0;
+#pragma unroll
+    for (int w = 0; w < 21; ++w) f ^= s.a[w].lo ^ s.a[w].hi;
+    dst[b * TW] = make_uint4(f, f, f, f);
+    cnt = 256;
+#else
+    compact_block<TW>(s, ring_all, rb, cnt, dst, pd);
+#endif
   }
+  xof_pend_store<TW>(pd, dst);
   return cnt;
 }
 
