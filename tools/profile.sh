@@ -12,7 +12,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
-  python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu "$@" > "$out/bench_trace.json" 2> "$out/trace.err"
+  python3 "$R/bench.py" --steps ${PROF_STEPS:-5} --warmup ${PROF_WARMUP:-1} --no-cpu "$@" > "$out/bench_trace.json" 2> "$out/trace.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o run -- \
   python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu --no-profile "$@" > "$out/bench_fetch.json" 2> "$out/fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o run -- \
