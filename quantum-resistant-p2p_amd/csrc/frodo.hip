@@ -235,6 +235,14 @@ __global__ __launch_bounds__(256) void k_fr_se_stream(const uint64_t* __restrict
   squeeze_tiled<P::RW>(s, raw, hs, W, RAWW);
 }
 
+// QRK_FR_SAMPLE_TILED 1: threads follow the tiled stream layout (coalesced reads, packed but
+// handshake-strided stores); 0 (default): one thread per (hs, word) in handshake order (strided
+// reads, stores contiguous across the wave).  A/B at FrodoKEM-640 2^16: 1.68-1.72 ms against
+// 1.40 ms (profiles/r2/ab_fr_sample_tiled_rejected.jsonl) -- the scattered stores cost more than
+// the scattered reads.
+#ifndef QRK_FR_SAMPLE_TILED
+#define QRK_FR_SAMPLE_TILED 0
+#endif
 // CDF sampler over the raw stream.  Encaps (KG=false): words -> S' (8N, int8 [8][NP]),
 // E' (8N, int16 [8][N]), E'' (64).  KeyGen (KG=true): S^T (8N -> int8 [8][NP]) and E (8N, int16 [N][8]).
 template <int N, bool KG>
@@ -245,6 +253,32 @@ __global__ __launch_bounds__(256) void k_fr_sample(const uint64_t* __restrict__ 
   constexpr int NV = KG ? 2 * N * NBAR : (2 * N + NBAR) * NBAR;  // 16-bit samples per hs
   constexpr int NW = NV / 4;
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;  // one u64 = 4 samples
+#if QRK_FR_SAMPLE_TILED
+  // thread t reads raw[t]: the tiled stream [C/64][W][64] in order, so a wave's read is 512
+  // contiguous bytes (64 handshakes, one word each); the 4 samples of a word are consecutive
+  // entries of one output row and leave as one 4-byte (S') or 8-byte (E', E'') store
+  static_assert(N % 4 == 0 && NW * 4 == NV, "a word's 4 samples stay in one row");
+  const size_t hs = ((t >> 6) / (size_t)RAWW) * 64 + (t & 63);
+  const int w = (int)((t >> 6) % (size_t)RAWW);
+  if (hs >= n || w >= NW) return;
+  const uint64_t x = raw[t];
+  int v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = cdf_sample<N>((uint32_t)(x >> (16 * e)) & 0xFFFF);
+  const int idx = 4 * w;
+  if (idx < NBAR * N) {
+    const int k = idx / N, j = idx % N;
+    *(uint32_t*)(sp8 + (hs * NBAR + k) * P::NP + j) =
+        (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 | (uint32_t)(uint8_t)v[2] << 16 | (uint32_t)(uint8_t)v[3] << 24;
+  } else {
+    const uint64_t q = (uint64_t)(uint16_t)v[0] | (uint64_t)(uint16_t)v[1] << 16 | (uint64_t)(uint16_t)v[2] << 32 |
+                       (uint64_t)(uint16_t)v[3] << 48;
+    if (idx < 2 * NBAR * N)
+      *(uint64_t*)(ep16 + hs * NBAR * N + (idx - NBAR * N)) = q;
+    else
+      *(uint64_t*)(epp16 + hs * 64 + (idx - 2 * NBAR * N)) = q;
+  }
+#else
   const size_t hs = t / NW;
   const int w = (int)(t % NW);
   if (hs >= n) return;
@@ -262,6 +296,7 @@ __global__ __launch_bounds__(256) void k_fr_sample(const uint64_t* __restrict__ 
       epp16[hs * 64 + (idx - 2 * NBAR * N)] = (int16_t)v;
     }
   }
+#endif
   // zero the K padding of S' rows once per hs (pad columns N..NP)
   if (w < NBAR && P::NP > N) {
     for (int j = N; j < P::NP; ++j) sp8[(hs * NBAR + w) * P::NP + j] = 0;
@@ -1270,7 +1305,7 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
     QRK_LAUNCH("k_fr_front_enc", st, k_fr_front_enc<N>, dim3(blocks_for(n)), dim3(256), 0, st, pk, mu, n, v.seeds);
   }
   launch_se<N>(v, n, 0x96, P::SE_WORDS, st);
-  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
+  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(round64(n) * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk, P::PK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
@@ -1288,7 +1323,7 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   QRK_LAUNCH("k_fr_dec_m", st, k_fr_dec_m<N>, dim3((unsigned)n), dim3(256), 0, st, n, ct, sk, v.seeds);
   QRK_LAUNCH("k_fr_g2_dec", st, k_fr_g2_dec<N>, dim3(blocks_for(n)), dim3(256), 0, st, sk, n, v.seeds);
   launch_se<N>(v, n, 0x96, P::SE_WORDS, st);
-  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(n * (P::SE_WORDS))), dim3(256), 0, st,
+  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(round64(n) * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk_in_sk, P::SK, n, st);
   QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
@@ -1307,7 +1342,7 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
              v.seeds);
   launch_se<N>(v, n, 0x5F, P::KG_WORDS, st);
   // S^T -> sp8 ([8][NP] int8), E -> ep16 as [N][8]
-  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(n * (P::KG_WORDS))), dim3(256), 0, st,
+  QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(round64(n) * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
   uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
   if (AES || !QRK_FR_KG_MM)
