@@ -402,28 +402,38 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 
 #endif
 
-// FIX == false: every entry squeezes exactly 3 blocks (uniform across the
-// wave); the ~0.7% that still lack 256 values append their index to `fix`.
-// FIX == true: one lane per listed entry recomputes it with as many blocks as
-// it needs (rewriting identical chunks), so the rare 4th block never idles a
-// whole wave.
-// One SampleNTT entry inst = (x K + y) C + hs: SHAKE128(rho || x || y), ALL = false: exactly 3
-// blocks (returns the count, < 256 when a 4th block is needed); ALL = true: as many blocks as it
-// takes.  rb = this lane's ring column (see compact_block).
-template <int K, bool ALL, int TW = 64>
-__device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, uint4* __restrict__ out,
-                                         char* ring_all, uint32_t rb) {
-  uint4* dst = out + (inst / TW) * 32 * TW + (inst % TW);
-  KState s;
+// QRK_XOF_RESUME 1: an entry that still lacks values after its 3 blocks saves its
+// sponge state, count and partial chunk (a 256-B record), and the fix-up resumes from there --
+// usually one more permutation -- instead of recomputing the entry from scratch (4+ sequential
+// permutations on a lane that is nearly alone on its SIMD).  Records are reserved for K^2 C / 16
+// entries (about 9x the expected 0.7 %); entries beyond that (e.g. a batch of keys chosen for
+// bad rho) go to the from-scratch list.  A/B on one box (profiles/r2/ab_xof_resume.jsonl): the
+// fix-up drops from 0.35 to 0.25 ms and stops slowing the front / decrypt kernels it overlaps,
+// but k_xof itself runs 1.8 % slower with the record path compiled in -- no net gain, so 0 is
+// the default (every fix-up entry recomputed from scratch, cap = 0).
+#ifndef QRK_XOF_RESUME
+#define QRK_XOF_RESUME 0
+#endif
+#if QRK_XOF_RESUME && QRK_XOF_ACC
+#error "QRK_XOF_RESUME restores the ring layout of the default compaction (QRK_XOF_ACC=0)"
+#endif
+constexpr int XOF_REC_WORDS = 64;  // [0] inst, [1] count, [2..51] state (lo, hi), [52..59] partial chunk
+__host__ __device__ inline size_t xof_rec_cap(int K, size_t C) { return (size_t)K * K * C / 16; }
+
+__device__ __forceinline__ void xof_init(KState& s, const uint64_t* __restrict__ rho, int xy, int K) {
   kzero(s);
 #pragma unroll
   for (int w = 0; w < 4; ++w) kxor(s, w, rho[w]);
   s.a[4].lo ^= (uint32_t)(xy / K) | ((uint32_t)(xy % K) << 8) | (DS_SHAKE << 16);
   s.a[RW_SHAKE128 - 1].hi ^= 0x80000000u;
-  int cnt = 0;
+}
+
+// squeeze + compact blocks: exactly NB of them (ALL = false), or until 256 values (ALL = true)
+template <bool ALL, int NB, int TW = 64>
+__device__ __forceinline__ void xof_blocks(KState& s, int& cnt, uint4* __restrict__ dst, char* ring_all, uint32_t rb) {
   XofPend pd;
 #pragma unroll 1
-  for (int b = 0; b < (ALL ? MAX_XOF_BLOCKS : 3) && (!ALL || cnt < 256); ++b) {
+  for (int b = 0; b < NB && (!ALL || cnt < 256); ++b) {
     keccak_f(s);
 #if QRK_XOF_TIMING_ONLY == 1
     // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
@@ -438,31 +448,91 @@ __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int x
 #endif
   }
   xof_pend_store<TW>(pd, dst);
+}
+
+// ring entry e (mod 16) of this lane (the default compaction's layout, see compact_block)
+__device__ __forceinline__ uint32_t* ring_entry(char* ring_all, uint32_t rb, int e) {
+  return (uint32_t*)(ring_all + ((uint32_t)(e & 15) << 8 | rb));
+}
+
+// One SampleNTT entry inst = (x K + y) C + hs from scratch: SHAKE128(rho || x || y), ALL = false:
+// exactly 3 blocks (returns the count, < 256 when a 4th block is needed); ALL = true: as many
+// blocks as it takes.  rb = this lane's ring column (see compact_block).
+template <int K, bool ALL, int TW = 64>
+__device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, uint4* __restrict__ out,
+                                         char* ring_all, uint32_t rb) {
+  uint4* dst = out + (inst / TW) * 32 * TW + (inst % TW);
+  KState s;
+  xof_init(s, rho, xy, K);
+  int cnt = 0;
+  xof_blocks<ALL, ALL ? MAX_XOF_BLOCKS : 3, TW>(s, cnt, dst, ring_all, rb);
   return cnt;
 }
 
+// FIX == false: every entry squeezes exactly 3 blocks (uniform across the wave); the ~0.7 % that
+// still lack 256 values get a fix-up slot (a resume record, or the from-scratch list past the cap).
+// FIX == true: one lane per slot completes the entry (rewriting identical chunks on the
+// from-scratch path), so the rare 4th block never idles a whole wave.
 template <int K, bool FIX>
 __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
                                              size_t n, size_t C, uint4* __restrict__ out,
-                                             uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix) {
+                                             uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix,
+                                             uint32_t* __restrict__ fixrec) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
 #if QRK_XOF_ACC
   const uint32_t rb = (threadIdx.x >> 7) * 8192 + ((threadIdx.x >> 6) & 1) * 256 + (threadIdx.x & 63) * 4;
 #else
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;
 #endif
-  const size_t stride = FIX ? (size_t)gridDim.x * 256 : 0;
-  size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const size_t limit = FIX ? (size_t)*nfix : (size_t)K * K * C;
+  char* ring = (char*)ring_all;
+  const size_t cap = QRK_XOF_RESUME ? xof_rec_cap(K, C) : 0;
+  if constexpr (!FIX) {
+    const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (inst >= (size_t)K * K * C || inst % C >= n) return;
+    KState s;
+    xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
+    int cnt = 0;
+    xof_blocks<false, 3>(s, cnt, out + (inst / 64) * 32 * 64 + (inst % 64), ring, rb);
+    if (cnt < 256) {
+      const size_t slot = atomicAdd(nfix, 1u);
+      if (slot < cap) {
+        uint32_t* rec = fixrec + slot * XOF_REC_WORDS;
+        rec[0] = (uint32_t)inst;
+        rec[1] = (uint32_t)cnt;
+#pragma unroll
+        for (int i = 0; i < 25; ++i) {
+          rec[2 + 2 * i] = s.a[i].lo;
+          rec[3 + 2 * i] = s.a[i].hi;
+        }
+        const int base = cnt & ~7;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (base + j < cnt) rec[52 + j] = *ring_entry(ring, rb, base + j);
+      } else {
+        fix[slot - cap] = (uint32_t)inst;
+      }
+    }
+  } else {
+    const size_t stride = (size_t)gridDim.x * 256, limit = (size_t)*nfix;
 #pragma unroll 1
-  for (; r < limit; r += stride) {
-    const size_t inst = FIX ? (size_t)fix[r] : r;
-    if (!FIX && inst % C >= n) return;
-    const int cnt = xof_entry<K, FIX>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst,
-                                      out, (char*)ring_all, rb);
-    if (!FIX) {
-      if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
-      return;
+    for (size_t r = (size_t)blockIdx.x * 256 + threadIdx.x; r < limit; r += stride) {
+      if (r < cap) {
+        const uint32_t* rec = fixrec + r * XOF_REC_WORDS;
+        const size_t inst = rec[0];
+        int cnt = (int)rec[1];
+        KState s;
+#pragma unroll
+        for (int i = 0; i < 25; ++i) s.a[i] = {rec[2 + 2 * i], rec[3 + 2 * i]};
+        const int base = cnt & ~7;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (base + j < cnt) *ring_entry(ring, rb, base + j) = rec[52 + j];
+        uint4* dst = out + (inst / 64) * 32 * 64 + (inst % 64);
+        xof_blocks<true, MAX_XOF_BLOCKS>(s, cnt, dst, ring, rb);
+      } else {
+        const size_t inst = fix[r - cap];
+        xof_entry<K, true>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring, rb);
+      }
     }
   }
 }
@@ -1192,9 +1262,11 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
+  uint32_t* fixrec;      // SampleNTT resume records (QRK_XOF_RESUME)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 2;
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 2 +
+         xof_rec_cap(K, C) * XOF_REC_WORDS / 2;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -1213,6 +1285,8 @@ inline ScratchView carve(void* base, int K, size_t C) {
   p += 4 * C;
   v.nfix = (uint32_t*)p;
   v.fix = v.nfix + 2;
+  p += ((size_t)K * K * C + 2) / 2 + 2;
+  v.fixrec = (uint32_t*)p;
   return v;
 }
 
@@ -1994,7 +2068,7 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
                 const Streams* fixside = nullptr) {
   (void)hipMemsetAsync(v.nfix, 0, 4, st);
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
-             C, (uint4*)v.xof, v.fix, v.nfix);
+             C, (uint4*)v.xof, v.fix, v.nfix, v.fixrec);
   hipStream_t fs = st;
   if (fixside) {
     (void)hipEventRecord(fixside->fork, st);
@@ -2006,8 +2080,7 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   // pass would double it
   const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
   QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C,
-             (uint4*)v.xof, v.fix,
-             v.nfix);
+             (uint4*)v.xof, v.fix, v.nfix, v.fixrec);
   if (fixside) (void)hipEventRecord(fixside->join, fs);
 }
 inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }

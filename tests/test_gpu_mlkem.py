@@ -247,3 +247,42 @@ def test_kat_records_through_single_shot_wrapper(golden_dir):
             h[k].update(v)
     for k in h:
         assert h[k].hexdigest() == g["digests"][k], k
+
+
+def _sample_ntt_needs_4th_block(rho: bytes, i: int, j: int) -> bool:
+    """FIPS 203 Alg. 7 acceptance count over the first 3 SHAKE128 blocks (504 bytes)."""
+    b = hashlib.shake_128(rho + bytes([j, i])).digest(504)
+    cnt = 0
+    for t in range(0, 504, 3):
+        d1 = b[t] | ((b[t + 1] & 0x0F) << 8)
+        d2 = (b[t + 1] >> 4) | (b[t + 2] << 4)
+        cnt += (d1 < 3329) + (d2 < 3329)
+    return cnt < 256
+
+
+@pytest.mark.parametrize("alg,k", [("ML-KEM-768", 3), ("ML-KEM-512", 2)])
+def test_sample_ntt_fixup_resume_and_overflow(engines, alg, k):
+    """Every pk of a 1100-handshake batch carries a rho whose matrix has entries that need a 4th
+    SHAKE128 block, so far more than K^2 C / 16 entries need the fix-up: the first ones resume
+    from their saved sponge state (QRK_XOF_RESUME records), the rest overflow to the
+    from-scratch list.  Encaps is byte-exact vs the oracle for every index."""
+    import oracle as orc
+    rng = np.random.default_rng(77 + k)
+    for _ in range(4000):
+        rho = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        bad = sum(_sample_ntt_needs_4th_block(rho, i, j) for i in range(k) for j in range(k))
+        if bad >= 1:
+            break
+    else:
+        pytest.fail("no rho with a 4-block SampleNTT entry found")
+    n = 1100  # > 1024: the batched schedule (k_xof + k_xof_fix)
+    coins = orc.bench_coins(n, 96, seed=4242)
+    kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
+    opk, _ = orc.batch_keypair(alg, kc[:1])
+    pk = np.repeat(opk, n, axis=0)
+    pk[:, -32:] = np.frombuffer(rho, dtype=np.uint8)
+    eng = engines[alg]
+    ct, ss = eng.encaps(_dev(pk), coins=_dev(ec))
+    oct_, oss = orc.batch_encaps(alg, pk, ec, 8)
+    assert np.array_equal(_host(ct), oct_)
+    assert np.array_equal(_host(ss), oss)
