@@ -179,10 +179,32 @@ __device__ __forceinline__ uint64_t kword(const KState& s, int i) {
 // NW is a compile-time constant so every state index is static.
 // The next block's words are loaded into registers before the current block's
 // permutation runs, so global-load latency hides behind the 24 rounds.
+// QRK_ABSORB_PREFETCH 1 (default): the next block's words are loaded into registers before the
+// current block's permutation (2 RW VGPRs more); 0: each block's words are loaded when absorbed
+// (latency left to the other resident waves, fewer VGPRs -> higher occupancy).  A/B: no faster for
+// ML-KEM (127 -> 82 VGPRs, 4 -> 5 waves / SIMD), slower for the FrodoKEM H(pk) and ss kernels
+// (profiles/r2/ab_absorb_prefetch.jsonl).
+#ifndef QRK_ABSORB_PREFETCH
+#define QRK_ABSORB_PREFETCH 1
+#endif
 template <int RW, int NW, uint32_t DS, typename Loader>
 __device__ __forceinline__ void absorb_words(KState& s, Loader ld) {
   constexpr int NFULL = NW / RW;
   constexpr int TAIL = NW % RW;
+#if !QRK_ABSORB_PREFETCH
+#pragma unroll 1
+  for (int b = 0; b < NFULL; ++b) {
+#pragma unroll
+    for (int w = 0; w < RW; ++w) kxor(s, w, ld(b * RW + w));
+    keccak_f(s);
+  }
+#pragma unroll
+  for (int w = 0; w < TAIL; ++w) kxor(s, w, ld(NFULL * RW + w));
+  s.a[TAIL].lo ^= DS;
+  s.a[RW - 1].hi ^= 0x80000000u;
+  keccak_f(s);
+  return;
+#endif
   uint64_t nxt[RW];
 #pragma unroll
   for (int w = 0; w < RW; ++w) nxt[w] = (NFULL > 0 || w < TAIL) ? ld(w) : 0;
