@@ -281,14 +281,19 @@ def cpu_baseline(alg, mode, kc, pk, sk, ec, ct_in, ss_gpu, B):
 
 
 def keccak_practical_peak():
-    """Top/s (4320-op count) of a register-resident Keccak-f[1600] loop measured on MI355X by
-    tools/valu_peak.hip (profiles/r1/valu_peak_r1b.json), or None."""
-    f = ROOT / "profiles" / "r1" / "valu_peak_r1b.json"
-    try:
-        d = json.loads(f.read_text())
-        return max(v for k, v in d.items() if k.startswith("keccak_") and k.endswith("_Tops_at_4320"))
-    except (OSError, ValueError):
-        return None
+    """Top/s (4320-op count) of a register-resident Keccak-f[1600] loop measured on MI355X: the
+    best of tools/valu_peak.hip (profiles/r1/valu_peak_r1b.json) and tools/rot64_probe.hip's
+    rounds-per-iteration variants (profiles/r2/rot64_unroll_probe.json, the kernels' two rounds
+    per iteration), or None."""
+    best = None
+    for f in (ROOT / "profiles" / "r1" / "valu_peak_r1b.json", ROOT / "profiles" / "r2" / "rot64_unroll_probe.json"):
+        try:
+            d = json.loads(f.read_text())
+            v = max(v for k, v in d.items() if k.startswith("keccak_") and k.endswith("_Tops_at_4320"))
+            best = v if best is None or v > best else best
+        except (OSError, ValueError):
+            pass
+    return best
 
 
 def pmc_traffic(alg, mode, chunk, kernel):
