@@ -171,6 +171,10 @@ def kernel_ops_per_hs(alg, name, mode):
         return ((pk + 1 + 135) // 136 + 1) * PERM_OPS, "valu"
     if name == "k_front_decaps":
         return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
+    if name == "k_j_decaps":  # J(z || c) alone (the side-stream half of k_front_decaps)
+        return ((32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
+    if name == "k_g_decaps":  # G(m' || h)
+        return PERM_OPS, "valu"
     if name == "k_prf":
         return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
     return None, None

@@ -688,6 +688,23 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
 }
+// The two halves of k_front_decaps as separate launches: J(z || c) needs only the inputs, so on the
+// single-stream schedule it runs on the side stream beside k_xof and the decrypt core
+// (QRK_J_SIDE); G(m' || h) follows the decrypt core on the main stream.
+template <int K>
+__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_j_decaps(const uint8_t* __restrict__ ct,
+                                                  const uint8_t* __restrict__ sk, size_t n, uint64_t* __restrict__ kbar) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  j_decaps_hs<K>(ct, sk, hs, kbar);
+}
+template <int K>
+__global__ __launch_bounds__(256) void k_g_decaps(const uint8_t* __restrict__ sk, const uint64_t* __restrict__ mprime,
+                                                  size_t n, uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime) {
+  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs >= n) return;
+  g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
+}
 template <int K>
 __global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk,
@@ -2060,6 +2077,10 @@ inline void join(const Streams& s) {
   (void)hipStreamWaitEvent(s.main, s.join, 0);
 }
 
+// QRK_J_SIDE 1: Decaps' J(z || c) on the side stream beside k_xof / the decrypt core (see k_j_decaps)
+#ifndef QRK_J_SIDE
+#define QRK_J_SIDE 0
+#endif
 // fixside: run the fix-up on Streams::side (the single-stream schedule's overlap of the
 // latency-bound fix-up with the next kernels on st); the caller joins with fix_join() before
 // the core reads the sampled matrix
@@ -2152,11 +2173,21 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   const Streams* fs = fix_side(s);
+  const bool jside = QRK_J_SIDE && fs;
+  if (jside) {  // J(z || c) on the side stream, after this chunk's predecessors on main (kbar reuse)
+    (void)hipEventRecord(fs->fork, st);
+    (void)hipStreamWaitEvent(fs->side, fs->fork, 0);
+    QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
+  }
   fork(s);
   launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd, fs);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
-             v.seeds, v.kprime, v.kbar);
+  if (jside)
+    QRK_LAUNCH("k_g_decaps", st, k_g_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, sk, v.mprime, n, v.seeds,
+               v.kprime);
+  else
+    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
+               v.seeds, v.kprime, v.kbar);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
              v.seeds, n, C, 2 * K + 1, K, v.prf);
   join(s);
