@@ -1,8 +1,9 @@
 // Wave-cooperative Keccak-f[1600] for gfx950: one sponge state spread over one wave.
 //
-// Used where one handshake's sponge chain is the critical path (the single-shot kernels: H(ek),
-// J(z || c), G, the PRFs and SampleNTT of one handshake), not for batches, where one state per
-// lane (keccak.cuh) keeps every lane busy.  One wave64 issues one VALU instruction per 4 cycles,
+// Used where one handshake's sponge chain is the critical path (the ML-KEM single-shot kernels:
+// H(ek), J(z || c), G, the PRFs and SampleNTT of one handshake; the FrodoKEM / HQC long sponges
+// below 256 handshakes: H(pk), the SE stream, ss, the seedexpanders and the K hash), not for large
+// batches, where one state per lane (keccak.cuh) keeps every lane busy.  One wave64 issues one VALU instruction per 4 cycles,
 // so the 4320-instruction lane-per-state permutation costs about 9 us on a single wave; spread
 // over the lanes it costs ~20 VALU + 10 lane permutes per round.
 //
