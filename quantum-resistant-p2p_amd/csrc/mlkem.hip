@@ -2077,7 +2077,10 @@ inline void join(const Streams& s) {
   (void)hipStreamWaitEvent(s.main, s.join, 0);
 }
 
-// QRK_J_SIDE 1: Decaps' J(z || c) on the side stream beside k_xof / the decrypt core (see k_j_decaps)
+// QRK_J_SIDE 1: Decaps' J(z || c) on the side stream beside k_xof / the decrypt core (see k_j_decaps).
+// Byte-exact (the ML-KEM GPU suite passes on it) but no faster: J stretches over k_xof and doubles
+// the decrypt core it overlaps, the chip being VALU-saturated either way
+// (profiles/r2/ab_j_side.jsonl); off by default.
 #ifndef QRK_J_SIDE
 #define QRK_J_SIDE 0
 #endif
