@@ -67,8 +67,27 @@ template <int L> struct HQ;
 // A/B on one box (2^16): HQC-128 (5, 128) for both beats (9, 64) + (5, 256); HQC-256 Encaps keeps
 // one position class (5, 384) while its Decaps gains from three (15, 128) (profiles/r1/ab_hqc_prod.txt)
 template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 5, 128, 5, 128, 256> {};
+// Threads per handshake for HQC-192 / 256 (A/B on one box, profiles/r2/ab_hqc_tpb.jsonl): HQC-256
+// runs 512 (3 workgroups x 8 waves per CU under its 52 KB of LDS, against 3 x 6 at 384): enc+dec
+// 3.81e6 -> 4.18e6 /s; HQC-192 stays at 256 (384 / 512 with three-word windows: 8.4e6 -> 7.25e6).
+#ifndef QRK_HQC192_TPB
+#define QRK_HQC192_TPB 256
+#endif
+#if QRK_HQC192_TPB == 512
+template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 3, 512, 512> {};
+#elif QRK_HQC192_TPB == 384
+template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 3, 384, 384> {};
+#else
 template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 5, 256, 256> {};
+#endif
+#ifndef QRK_HQC256_TPB
+#define QRK_HQC256_TPB 512
+#endif
+#if QRK_HQC256_TPB == 512
+template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 512, 512> {};
+#else
 template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 384, 384> {};
+#endif
 
 // ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
 struct alignas(4) GfTabs {
