@@ -76,7 +76,8 @@ template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 5, 12
 #endif
 // Threads per handshake for HQC-192 / 256 (A/B on one box, profiles/r2/ab_hqc_tpb.jsonl): HQC-256
 // runs 512 (3 workgroups x 8 waves per CU under its 52 KB of LDS, against 3 x 6 at 384): enc+dec
-// 3.81e6 -> 4.18e6 /s; HQC-192 stays at 256 (384 / 512 with three-word windows: 8.4e6 -> 7.25e6),
+// 3.81e6 -> 4.18e6 /s; HQC-192 stays at 256 (384 / 512 with three-word windows: 8.4e6 -> 7.25e6;
+// 384 with five-word windows, 35.7 KB of LDS: 6.2e6),
 // and so does HQC-128 (512: 17.2e6 -> 15.0e6; it already holds the 32-wave limit at 256).
 #ifndef QRK_HQC192_TPB
 #define QRK_HQC192_TPB 256
