@@ -417,6 +417,15 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
 #if QRK_XOF_RESUME && QRK_XOF_ACC
 #error "QRK_XOF_RESUME restores the ring layout of the default compaction (QRK_XOF_ACC=0)"
 #endif
+// QRK_XOF_TW: tile width of the batched SampleNTT output (chunk c of entry i at
+// ((i / XTW) 32 + c) XTW + i % XTW, 16-byte units): 64 (default) makes k_xof's stores one
+// contiguous KB per wave; 1 makes each entry's 512 B contiguous for the cores' 16-lane reads.
+// A/B (profiles/r2/ab_xof_tile_width.jsonl): 1 speeds the encrypt core up 4 % but slows k_xof's
+// scattered 16-byte stores 4-8 % (net -2 %); 8 is even with 64.
+#ifndef QRK_XOF_TW
+#define QRK_XOF_TW 64
+#endif
+constexpr int XTW = QRK_XOF_TW;
 constexpr int XOF_REC_WORDS = 64;  // [0] inst, [1] count, [2..51] state (lo, hi), [52..59] partial chunk
 __host__ __device__ inline size_t xof_rec_cap(int K, size_t C) { return (size_t)K * K * C / 16; }
 
@@ -492,7 +501,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
     KState s;
     xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
     int cnt = 0;
-    xof_blocks<false, 3>(s, cnt, out + (inst / 64) * 32 * 64 + (inst % 64), ring, rb);
+    xof_blocks<false, 3, XTW>(s, cnt, out + (inst / XTW) * 32 * XTW + (inst % XTW), ring, rb);
     if (cnt < 256) {
       const size_t slot = atomicAdd(nfix, 1u);
       if (slot < cap) {
@@ -527,11 +536,12 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (base + j < cnt) *ring_entry(ring, rb, base + j) = rec[52 + j];
-        uint4* dst = out + (inst / 64) * 32 * 64 + (inst % 64);
-        xof_blocks<true, MAX_XOF_BLOCKS>(s, cnt, dst, ring, rb);
+        uint4* dst = out + (inst / XTW) * 32 * XTW + (inst % XTW);
+        xof_blocks<true, MAX_XOF_BLOCKS, XTW>(s, cnt, dst, ring, rb);
       } else {
         const size_t inst = fix[r - cap];
-        xof_entry<K, true>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring, rb);
+        xof_entry<K, true, XTW>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring,
+                                rb);
       }
     }
   }
@@ -1365,7 +1375,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)(j * K) * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K) * C + hss, L);
   CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
@@ -1377,7 +1387,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)(j * K + i + 1) * C + hss, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K + i + 1) * C + hss, L);
       er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
     }
     PF16 ef;
@@ -1444,7 +1454,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 #if QRK_ENC_PREFETCH
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)j * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)j * C + hss, L);
 #endif
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
@@ -1457,13 +1467,13 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
 #else
 #pragma unroll
-    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW>((const uint4*)xof, (size_t)(i * K + j) * C + hss, L), yb[j]);
+    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(i * K + j) * C + hss, L), yb[j]);
 #endif
     const CbdRaw ecur = er;
 #if QRK_ENC_PREFETCH
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hss, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hss, L);
     }
 #endif
     er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
