@@ -710,6 +710,45 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   }
 }
 
+// QRK_HQC_NOMB 1: both doubled operands built in place from raw words staged at the front of D1 / D2
+// (every thread reads first, one barrier, then the stores), so enc_mul needs no separate staging /
+// message buffer and its LDS footprint drops by MBW words (more workgroups per CU for HQC-192/256).
+#ifndef QRK_HQC_NOMB
+#define QRK_HQC_NOMB 1
+#endif
+template <int L>
+__device__ __forceinline__ void build_doubled2_inplace(uint32_t* D1, uint32_t* D2) {
+  using P = HQ<L>;
+  constexpr uint32_t TOPMASK = (1u << P::NR) - 1;
+  constexpr int QPT = (P::NH2 + P::TPB - 1) / P::TPB;
+  const int tq = hq_tid();
+  uint32_t a[QPT], b[QPT];
+#pragma unroll
+  for (int k = 0; k < QPT; ++k) {
+    const int q = tq + k * P::TPB;
+    uint32_t va = 0, vb = 0;
+    if (q < P::NH2) {
+      if (q < P::NW32) va = D1[q], vb = D2[q];
+      if (q >= P::N32) {
+        const int j1 = q - P::N32, j0 = j1 - 1;  // j1 < NW32 always; j0 may be -1
+        uint32_t h1 = j1 < P::NW32 ? D1[j1] : 0u, s1 = j1 < P::NW32 ? D2[j1] : 0u;
+        uint32_t h0 = j0 >= 0 ? D1[j0] : 0u, s0 = j0 >= 0 ? D2[j0] : 0u;
+        if (j1 == P::NW32 - 1) h1 &= TOPMASK, s1 &= TOPMASK;
+        if (j0 == P::NW32 - 1) h0 &= TOPMASK, s0 &= TOPMASK;
+        va ^= alignbit(h1, h0, 32 - P::NR);
+        vb ^= alignbit(s1, s0, 32 - P::NR);
+      }
+    }
+    a[k] = va, b[k] = vb;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < QPT; ++k) {
+    const int q = tq + k * P::TPB;
+    if (q < P::NH2) D1[q] = a[k], D2[q] = b[k];
+  }
+}
+
 // QRK_HQC_DPP_WIN 1: each window's last word from the neighbouring lane by DPP wave_shl:1 (one LDS
 // read fewer per window); A/B slower (HQC-128 enc_mul 0.818 vs 0.766 ms, HQC-256 6.18 vs 4.98 ms,
 // profiles/r2/ab_hqc_dpp_win_rejected.jsonl), off by default
@@ -899,6 +938,12 @@ __device__ unsigned long long g_hqc_trace[32];
 #ifndef QRK_HQC_WPE
 #define QRK_HQC_WPE 8
 #endif
+#ifndef QRK_HQC_WPE192  // 72 VGPRs: 7 waves / SIMD, which the NOMB LDS footprint (21.5 KB) allows
+#define QRK_HQC_WPE192 7
+#endif
+#ifndef QRK_HQC_WPE256  // 64 VGPRs: 8 waves / SIMD = four 512-thread workgroups (37.6 KB LDS each)
+#define QRK_HQC_WPE256 8
+#endif
 #ifndef QRK_HQC_WG_PER_CU
 #define QRK_HQC_WG_PER_CU 8
 #endif
@@ -963,20 +1008,26 @@ __device__ __forceinline__ void enc_issue(EncIn<L, REENC>& in, size_t hs, const 
 // 8 waves per SIMD at HQC-128 as before the loop (<= 64 VGPRs; HQC-192/256 are held to 5 by their
 // LDS): without the bound the compiler keeps loop-invariant values live across the handshake loop
 template <int L, bool REENC>
-__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 128 ? QRK_HQC_WPE : 5))) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 128 ? QRK_HQC_WPE : (L == 192 ? QRK_HQC_WPE192 : QRK_HQC_WPE256)))) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
                                                      const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ ct_out, const uint8_t* __restrict__ mp,
                                                      const uint8_t* __restrict__ sk, const uint8_t* __restrict__ ct_in,
                                                      int32_t* __restrict__ status, uint64_t* __restrict__ msg) {
   using P = HQ<L>;
-  __shared__ uint32_t D1[P::NH2], D2[P::NH2];
-  __shared__ __attribute__((aligned(16))) uint32_t MB[P::MBW];
+  // NOMB: the message is assembled over u (D1) once u has been read out (HQC-128 is wave-limited,
+  // not LDS-limited, and keeps the separate buffer: the in-place path costs it a spill at 64 VGPRs)
+  constexpr bool NOMB = QRK_HQC_NOMB && L != 128;
+  __shared__ __attribute__((aligned(16))) uint32_t D1[P::NH2];
+  __shared__ uint32_t D2[P::NH2];
+  __shared__ __attribute__((aligned(16))) uint32_t MBX[NOMB ? 4 : P::MBW];
+  uint32_t* const MB = NOMB ? D1 : MBX;
+  static_assert(!NOMB || (2 * P::MW <= P::NH2 && P::K / 4 + (P::NB + P::VB + 3) / 4 <= P::NH2), "message fits D1");
+  static_assert(NOMB || 2 * P::NW32 <= P::MBW, "raw h and s words fit the message buffer");
   __shared__ uint32_t SS[3 * P::WMAX];
   uint32_t* const S1 = SS;
   uint32_t* const S2 = SS + P::WMAX;
   uint32_t* const SE = SS + 2 * P::WMAX;
   static_assert(P::WR == P::WE, "one dedupe over r1, r2, e");
-  static_assert(2 * P::NW32 <= P::MBW, "raw h and s words fit the message buffer");
   __shared__ __attribute__((aligned(4))) uint8_t GE[512], GL[256];
   __shared__ uint8_t SYM[128], MM[32];
   __shared__ uint32_t DIFF;
@@ -998,8 +1049,9 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
     for (int k = 0; k < EncIn<L, REENC>::WA; ++k) {
       const int j = t + k * P::TPB;
       if (j < P::NW32) {
-        MB[j] = ld32_finish(in.sw[k], in.ssh, j, P::NB);
-        MB[P::NW32 + j] = j == P::NW32 - 1 ? in.h[k] & ((1u << P::NR) - 1) : in.h[k];
+        uint32_t* const dst = NOMB ? D2 : MB;  // raw s, then raw h
+        dst[j] = ld32_finish(in.sw[k], in.ssh, j, P::NB);
+        (NOMB ? D1 : MB + P::NW32)[j] = j == P::NW32 - 1 ? in.h[k] & ((1u << P::NR) - 1) : in.h[k];
       }
     }
     if (t < P::WR) S1[t] = (uint32_t)t + __umulhi(in.q1, (uint32_t)(P::N - t));
@@ -1011,8 +1063,12 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
     HQ_MARK(1 + 8 * REENC);
     if (QRK_HQC_PERSIST && hs + hstep < n) enc_issue<L, REENC>(in, hs + hstep, row, coins, pk, mp, sk);
     // phase B: RS parity (wave 3), the three duplicate removals on waves 0-2
-    build_doubled<L>(D1, [&](int j) { return MB[P::NW32 + j]; });
-    build_doubled<L>(D2, [&](int j) { return MB[j]; });
+    if constexpr (NOMB) {
+      build_doubled2_inplace<L>(D1, D2);
+    } else {
+      build_doubled<L>(D1, [&](int j) { return MB[P::NW32 + j]; });
+      build_doubled<L>(D2, [&](int j) { return MB[j]; });
+    }
     HQ_MARK_T(24 + 4 * REENC, 0);
     if (wave == 0) dedupe_wave<P::WR>(S1);
     HQ_MARK_T(25 + 4 * REENC, 0);
@@ -1056,8 +1112,27 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
       const int sym = j / (4 * P::MULT);
       return D2[j] ^ rm_word(SYM[sym], j & 3);
     };
+    // NOMB: u (in D1) out to registers before the message is built over it
+    constexpr int UPT = (P::NW32 + P::TPB - 1) / P::TPB;
+    uint32_t uw[UPT];
+    if constexpr (NOMB) {
+#pragma unroll
+      for (int k = 0; k < UPT; ++k) {
+        const int j = t + k * P::TPB;
+        uw[k] = j < P::NW32 ? (j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j]) : 0u;
+      }
+      __syncthreads();
+    }
     if constexpr (!REENC) {
-      for (int j = t; j < P::NW32; j += P::TPB) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
+      if constexpr (NOMB) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+          const int j = t + k * P::TPB;
+          if (j < P::NW32) MB[UOFF + j] = uw[k];
+        }
+      } else {
+        for (int j = t; j < P::NW32; j += P::TPB) MB[UOFF + j] = j == P::NW32 - 1 ? (D1[j] & TOPMASK) : D1[j];
+      }
       if (t < P::K) mb[t] = MM[t];
       __syncthreads();  // the last u word's spare bytes are v's first bytes
       for (int j = t; j < P::VW32; j += P::TPB) lds_store_u32_unaligned(mb, P::K + P::NB + 4 * j, vword(j));
@@ -1068,15 +1143,23 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
       for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[P::K / 4 + j] = ld32_masked(cin, j, P::NB + P::VB);
       __syncthreads();
       uint32_t diff = 0;
-      for (int j = t; j < P::NW32; j += P::TPB) {
-        uint32_t u = D1[j], c = MB[UOFF + j];
-        if (j == P::NW32 - 1) {
-          u &= TOPMASK;
-          constexpr int VALID = P::NB - 4 * (P::NW32 - 1);  // bytes of the last word that belong to u
-          constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
-          c &= BM;
+      constexpr int VALID = P::NB - 4 * (P::NW32 - 1);  // bytes of the last word that belong to u
+      constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
+      if constexpr (NOMB) {
+#pragma unroll
+        for (int k = 0; k < UPT; ++k) {
+          const int j = t + k * P::TPB;
+          if (j < P::NW32) diff |= uw[k] ^ (j == P::NW32 - 1 ? MB[UOFF + j] & BM : MB[UOFF + j]);
         }
-        diff |= u ^ c;
+      } else {
+        for (int j = t; j < P::NW32; j += P::TPB) {
+          uint32_t u = D1[j], c = MB[UOFF + j];
+          if (j == P::NW32 - 1) {
+            u &= TOPMASK;
+            c &= BM;
+          }
+          diff |= u ^ c;
+        }
       }
       for (int j = t; j < P::VW32; j += P::TPB) diff |= vword(j) ^ lds_u32_unaligned(mb, P::K + P::NB + 4 * j);
       if (diff) atomicOr(&DIFF, 1u);
