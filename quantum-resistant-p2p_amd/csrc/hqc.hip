@@ -1233,14 +1233,28 @@ __device__ __forceinline__ uint32_t max_wave(uint32_t k) {
 }
 
 // ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
+// QRK_HQC_DEC_ALIAS 1: the combined product T reuses the u || v staging buffer (v is folded into
+// the partial sums before the combine), one barrier more and NWP words less LDS per workgroup
+#ifndef QRK_HQC_DEC_ALIAS
+#define QRK_HQC_DEC_ALIAS 1
+#endif
+#ifndef QRK_HQC_DEC_WPE  // HQC-192 (56 VGPRs); HQC-128 / 256 fit 8 waves unconstrained (256 spills when pinned)
+#define QRK_HQC_DEC_WPE 8
+#endif
 template <int L>
-__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 192 ? QRK_HQC_DEC_WPE : 1))) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ ct, uint8_t* __restrict__ syms,
                                                     size_t sym_stride) {
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2];
+  constexpr int MBD = (P::NB + P::VB + 8) / 4 + 1;
+#if QRK_HQC_DEC_ALIAS
+  __shared__ uint32_t MB[MBD > P::NWP ? MBD : P::NWP];
+  uint32_t* const T = MB;
+#else
   __shared__ uint32_t T[P::NWP];
-  __shared__ uint32_t MB[(P::NB + P::VB + 8) / 4 + 1];
+  __shared__ uint32_t MB[MBD];
+#endif
   __shared__ uint32_t SY[P::WMAX];
   __shared__ uint8_t SYM[128];
   const size_t hs = blockIdx.x;
@@ -1287,6 +1301,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_decode(size_t n, const uint6
 #pragma unroll
     for (int q = 0; q < P::WPT; ++q) acc[0][q] = j0 + q < P::VW32 ? acc[0][q] : 0u;
   }
+  if (QRK_HQC_DEC_ALIAS) __syncthreads();  // every v read done before T overwrites it
   uint32_t* const outs[1] = {T};
   prod_combine<1, P::WPT, P::NBT>(outs, acc, [] {});
   HQ_MARK(20);
