@@ -626,6 +626,81 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
     if (64 * e + lane < WT) s[64 * e + lane] = (x[e] & REP) ? (uint32_t)(64 * e + lane) : v[e];
 }
 
+// QRK_HQC_DEDUPE_WG 1: the closed form's first term spread over all NWV waves of the workgroup
+// (wave w takes j = w mod NWV, its ballot masks OR-ed into DUP in LDS), the chain on wave 0 --
+// for Decaps' single dedupe, where the other waves would otherwise wait at the barrier.
+// DUP[2 NE] zeroed and s visible before the call; every thread of the workgroup calls it.
+// Off by default: shorter per-handshake latency, but throughput-neutral with 8 waves per SIMD
+// resident (profiles/r2/ab_hqc_dedupe_wg_rejected.jsonl).
+#ifndef QRK_HQC_DEDUPE_WG
+#define QRK_HQC_DEDUPE_WG 0
+#endif
+template <int WT, int NWV>
+__device__ __forceinline__ void dedupe_wg(uint32_t* s, uint32_t* DUP) {
+  constexpr int NE = (WT + 63) / 64;
+  constexpr uint32_t NONE = 0xFFFFu, REP = 0x80000000u;
+  constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);
+  static_assert(NE <= 3 && WT > 1, "weight");
+  const int tq = hq_tid(), lane = tq & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tq >> 6);
+  uint32_t v[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
+  uint64_t dup[NE] = {};
+#pragma unroll
+  for (int j = 1; j < WT; ++j) {
+    if (j % NWV != wv) continue;  // wave-uniform
+    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      if (64 * e >= j) continue;
+      uint64_t m = __ballot(v[e] == sj);
+      if (64 * e + 64 > j) m &= (1ull << (j - 64 * e)) - 1;
+      dup[e] |= m;
+    }
+  }
+  if (lane < 2 * NE) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      w = lane == 2 * e ? (uint32_t)dup[e] : w;
+      w = lane == 2 * e + 1 ? (uint32_t)(dup[e] >> 32) : w;
+    }
+    if (w) atomicOr(&DUP[lane], w);
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  uint32_t x[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const uint32_t i = 64 * e + lane;
+    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
+    const uint32_t dw = DUP[2 * e + (lane >> 5)];
+    x[e] = ((dw >> (lane & 31)) & 1 ? REP : 0u) | ptr;
+  }
+#pragma unroll 1
+  for (int r = 0; r < ROUNDS; ++r) {
+    uint32_t y[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const uint32_t p = x[e] & NONE;
+      const int src = 4 * (int)(p & 63);
+      uint32_t g = 0;
+#pragma unroll
+      for (int f = 0; f < NE; ++f) {
+        const uint32_t gf = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)x[f]);
+        g = (p >> 6) == (uint32_t)f ? gf : g;
+      }
+      y[e] = p == NONE ? x[e] : ((x[e] & REP) | g);
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) x[e] = y[e];
+  }
+#pragma unroll
+  for (int e = 0; e < NE; ++e)
+    if (64 * e + lane < WT) s[64 * e + lane] = (x[e] & REP) ? (uint32_t)(64 * e + lane) : v[e];
+}
+
 // The spec's loop itself on one wave: step i (w-2 .. 0) broadcasts s_i (v_readlane), compares it
 // with every current s_j (a ballot per register, masked to j > i) and replaces s_i by i on a hit
 // (a wave-uniform decision): w - 1 dependent steps.
@@ -1256,6 +1331,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
   __shared__ uint32_t MB[MBD];
 #endif
   __shared__ uint32_t SY[P::WMAX];
+  __shared__ uint32_t DUP[6];
   __shared__ uint8_t SYM[128];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
@@ -1276,12 +1352,16 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
 #endif
   for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::NB + P::VB);
   supports_raw<L>(rw + P::RWW, P::W, SY);
+  if (t < 6) DUP[t] = 0;
   __syncthreads();
 #if !QRK_HQC_GDOUBLED
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? (MB[j] & BM) : MB[j]; });
 #endif
   HQ_MARK(17);
-  if (wave == 0) dedupe_wave<P::W>(SY);
+  if (QRK_HQC_DEDUPE_WG)
+    dedupe_wg<P::W, P::TPB / 64>(SY, DUP);
+  else if (wave == 0)
+    dedupe_wave<P::W>(SY);
   __syncthreads();
   HQ_MARK(18);
   uint32_t acc[1][P::WPT] = {};
