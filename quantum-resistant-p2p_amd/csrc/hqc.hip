@@ -922,8 +922,13 @@ __device__ __forceinline__ void fill_gf(uint8_t* e, uint8_t* l) {
 }
 
 // ---------------------------------------------------------------- KeyGen: s = x + y h
+// QRK_HQC_KG_WPE: waves_per_eu pin for HQC-256's KeyGen product (0: unpinned, 107 VGPRs, 4 waves
+// per SIMD; 6: 76 VGPRs, no spill, 6 waves; 8 spills 92 B).  Not yet measured on the GPU: off.
+#ifndef QRK_HQC_KG_WPE
+#define QRK_HQC_KG_WPE 0
+#endif
 template <int L>
-__global__ __launch_bounds__(HQ<L>::TPB) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 256 && QRK_HQC_KG_WPE ? QRK_HQC_KG_WPE : 1))) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ coins, uint8_t* __restrict__ pk,
                                                     uint8_t* __restrict__ sk) {
   using P = HQ<L>;
