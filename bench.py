@@ -11,7 +11,9 @@ collective; one all_reduce of counters + max elapsed at the end).
 
 python bench.py [--gpus N --steps K --warmup W] [--alg ML-KEM-768] [--log2-batch 20]
                 [--mode encdec|decaps-tampered] [--no-cpu]
-For N > 1 launch with torch.distributed.run (one rank per GPU, RCCL backend).
+For N > 1 bench.py either runs under torch.distributed.run (one rank per GPU, RCCL backend) or,
+started directly with --gpus N, launches the N ranks itself as a child process and relays rank 0's
+line.
 """
 from __future__ import annotations
 
@@ -138,6 +140,36 @@ def hqc_work(alg):
                     "k_hqc_kg_mul": w * nw32 * SPARSE_OPS}}
 
 
+# ML-KEM polynomial cores: per-stage lane-instruction counts of the minimal gfx950 sequence for
+# each stage as the cores implement it (DESIGN.md "Pricing the polynomial cores"); FIPS 203
+# Alg. 9-12 plus CBD, compress and the byte codecs.
+FWD_NTT = 7 * 128 * 6              # fp32 butterfly: v_mul, v_fmamk, v_sub (magic), v_fma, v_add, v_sub
+INV_NTT = 7 * 128 * 6 + 2 * 128 * 3 + 256 * 4  # + the two reduced sum layers + the 128^-1 scaling modmul
+NTT_MIDRED = 256 * 3               # decrypt: inputs up to q, one reduction after layer 4
+CBD_OPS = {2: 256 * 3, 3: 256 * 4}  # SWAR nibble sums + fp32 conversion per coefficient
+BOP = 128 * 10                     # basemul operand (b0, b1*gamma) / (b1, b0) from an NTT output
+BMUL = 128 * 2                     # one (row, j) term: two v_dot2c_i32_i16 per coefficient pair
+ACC = 256 * 8                      # int32 accumulator -> centered fp32 residue (acc_to_f)
+COMPRESS = 256 * 6                 # canonicalise + Compress_d (mulhi) per coefficient
+DEC12 = 256 * 2                    # ByteDecode_12 + the FIPS 203 7.2 modulus reduction
+ENC12 = 256 * 3                    # canonicalise + ByteEncode_12
+UNPACK = 256 * 5                   # ByteDecode_d + Decompress_d per coefficient
+PACK = 256 * 2                     # ByteEncode_d per coefficient
+DEC_MSG = 256 * 8                  # Decaps: Decompress_dv(v) - w, canonicalise, Compress_1
+
+
+def mlkem_core_ops(k, eta1, kind):
+    """Algorithmic lane-ops per handshake of one launch of an ML-KEM polynomial core."""
+    if kind == "encrypt":  # K-PKE.Encrypt (Encaps, and the Decaps re-encryption)
+        return (k * CBD_OPS[eta1] + (k + 1) * CBD_OPS[2] + k * FWD_NTT + k * BOP + (k * k + k) * BMUL
+                + (k + 1) * (ACC + INV_NTT + COMPRESS + PACK) + k * DEC12)
+    if kind == "decrypt":  # K-PKE.Decrypt
+        return (k + 1) * UNPACK + k * (FWD_NTT + NTT_MIDRED + DEC12 + BOP + BMUL) + ACC + INV_NTT + DEC_MSG
+    if kind == "keygen":   # K-PKE.KeyGen: s, e sampling + NTT, t = A s + e, both encodings
+        return 2 * k * (CBD_OPS[eta1] + FWD_NTT) + k * BOP + k * k * BMUL + k * ACC + 3 * k * ENC12
+    raise ValueError(kind)
+
+
 def kernel_ops_per_hs(alg, name, mode):
     """Algorithmic ops one handshake contributes to kernel `name` in one bench step
     (encaps+decaps, or decaps only) and the bound they are priced against."""
@@ -177,6 +209,12 @@ def kernel_ops_per_hs(alg, name, mode):
         return PERM_OPS, "valu"
     if name == "k_prf":
         return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
+    if name == "k_encrypt_core":  # Encaps' Encrypt, and Decaps' re-encryption
+        return calls * mlkem_core_ops(k, eta1, "encrypt"), "valu"
+    if name == "k_decrypt_core":
+        return mlkem_core_ops(k, eta1, "decrypt"), "valu"
+    if name == "k_keygen_core":
+        return mlkem_core_ops(k, eta1, "keygen"), "valu"
     return None, None
 
 
@@ -269,6 +307,15 @@ def cpu_baseline(alg, mode, kc, pk, sk, ec, ct_in, ss_gpu, B):
         orc.decaps_rc(alg, osk[m].tobytes(), cc)
         m += 1
     single = m / (time.perf_counter() - t0)
+    # KeyGen one call at a time on one core: the protocol runs it twice per exchange
+    # (messaging.py:590, 809; key_exchange.py:133)
+    kc_s = take(kc, min(S, 4096))
+    t0 = time.perf_counter()
+    m_kg = 0
+    while time.perf_counter() - t0 < 1.0 and m_kg < kc_s.shape[0]:
+        orc.keypair(alg, kc_s[m_kg].tobytes())
+        m_kg += 1
+    single_kg = m_kg / (time.perf_counter() - t0)
     spec = "FrodoKEM round 3" if alg in FP else ("HQC 2023-04-30" if alg in HQ else "FIPS 203")
     return {
         "value": S / dt, "unit": "encaps+decaps/s" if mode == "encdec" else "decaps/s", "cores": threads,
@@ -281,6 +328,8 @@ def cpu_baseline(alg, mode, kc, pk, sk, ec, ct_in, ss_gpu, B):
         "keygen_sample_matches_gpu": keygen_match,
         "keygen_per_s": keygen_rate,
         "single_core_python_per_call": single,
+        "single_core_python_keygen_per_call": single_kg,
+        "single_core_python_keygen_us_per_call": 1e6 / single_kg,
     }
 
 
@@ -659,6 +708,71 @@ def _ctx_profile_read(obj):
     return out
 
 
+def launcher_argv(bench_argv, nproc, port, script=None):
+    """The child command that runs this bench as `nproc` ranks (one per GPU) when bench.py is
+    started without a launcher: torch.distributed.run on 127.0.0.1, same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(script or ROOT / "bench.py"), *bench_argv]
+
+
+def launcher_env(environ):
+    """Environment of the launched ranks: the caller's, with dmabuf IPC kept (RCCL on this image
+    needs HSA_ENABLE_IPC_MODE_LEGACY=0) and no stale rank variables."""
+    env = {k: v for k, v in environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def pick_json_line(text):
+    """The single result line rank 0 printed (the last stdout line that parses as a bench JSON)."""
+    found = None
+    for line in text.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            if isinstance(d, dict) and "metric" in d and "value" in d:
+                found = line
+    return found
+
+
+def launch_ranks(nproc, bench_argv, script=None):
+    """--gpus N > 1 without WORLD_SIZE: start the N ranks as a child process (this process has
+    made no HIP call, and it never execs), relay rank 0's JSON line, exit with the child's code."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    proc = subprocess.run(launcher_argv(bench_argv, nproc, port, script), env=launcher_env(os.environ),
+                          stdout=subprocess.PIPE, text=True)
+    line = pick_json_line(proc.stdout)
+    if line is not None:
+        print(line)
+    elif proc.stdout:
+        sys.stdout.write(proc.stdout)
+    if proc.returncode == 0 and line is None:
+        return 1
+    return proc.returncode
+
+
+def strong_digest_block(world, total):
+    """Block of global indices for the strong-scaling shard digests: 2^20 (one library chunk)
+    when every shard boundary falls on it, else the largest divisor of 2^20 that every boundary
+    shares; None when that is below 2^12 (then one digest per rank is reported instead)."""
+    import math
+
+    from qrkem.shard import DIGEST_BLOCK, strong_shard
+    g = DIGEST_BLOCK
+    for r in range(world):
+        g = math.gcd(g, strong_shard(r, world, total).first)
+    g = math.gcd(g, total)
+    return g if g >= 1 << 12 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -679,6 +793,10 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
+    if args.global_log2_batch is not None and (1 << args.global_log2_batch) < args.gpus:
+        raise SystemExit(f"--global-log2-batch {args.global_log2_batch}: fewer handshakes than ranks")
+    if os.environ.get("WORLD_SIZE") in (None, "") and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])  # before any HIP call: no exec, a child
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
     local = env_int("LOCAL_RANK", 0)
@@ -705,8 +823,7 @@ def main():
     if args.mode == "wire":
         return bench_wire(args, world, rank, local)
     from qrkem.batch import BatchKEM
-    from qrkem.shard import DIGEST_BLOCK, block_digests, combine_digests, gather_digests, reduce_run, \
-        strong_shard, weak_shard
+    from qrkem.shard import block_digests, combine_digests, gather_digests, reduce_run, strong_shard, weak_shard
     alg = args.alg
     frodo = alg in FP
     hqc = alg in HQ
@@ -787,8 +904,9 @@ def main():
     elapsed, out = timed(main_step, profile=not args.no_profile)
     prof_live = eng.profile_read() if not args.no_profile else {}
     eng.profile(False)
-    # Kernel-in-isolation pass (serial schedule, one untimed step): the forked
-    # schedule overlaps kernel chains, which inflates per-kernel event durations.
+    # Kernel-in-isolation pass (serial schedule, one untimed step: qrk_ctx_set_streams(1) runs
+    # every kernel of an operation on the caller's stream, the SampleNTT fix-up included), since
+    # overlapping kernels stretch each other's event spans.
     prof = {}
     if not args.no_profile:
         eng.set_streams(1)
@@ -884,7 +1002,7 @@ def main():
         "valu_ops_per_unit": W,
         "keygen_per_s": B * world / keygen_s if keygen_s > 0 else None,
         "kernels": kernels,
-        "kernels_timed_region_forked": {k: {"avg_ms": ms / c, "launches": c} for k, (ms, c) in prof_live.items()},
+        "kernels_timed_region": {k: {"avg_ms": ms / c, "launches": c} for k, (ms, c) in prof_live.items()},
         "checks": checks,
         "cpu_baseline": None,
     }
@@ -892,11 +1010,17 @@ def main():
         # per-record SHA3-256(ct_i || ss_i) on the GPU, SHA-256 per block of 2^20 global indices:
         # the same block digests for every GPU count
         recs = eng.digest_rows(ct, ss).cpu().numpy()
-        mine = block_digests(recs, base)
+        dblock = strong_digest_block(world, 1 << lb)
+        if dblock is not None:
+            mine = block_digests(recs, base, dblock)
+        else:  # shards not aligned to any block of >= 2^12 indices: one digest per rank
+            import hashlib
+            mine = {rank: hashlib.sha256(np.ascontiguousarray(recs).tobytes()).hexdigest()}
         allb = gather_digests(mine)
         result["shard_digests"] = {
-            "record": "SHA3-256(ct_i || ss_i)", "block": DIGEST_BLOCK,
-            "block_digest": "SHA-256 over the block's record digests in index order",
+            "record": "SHA3-256(ct_i || ss_i)", "block": dblock if dblock is not None else "per-rank",
+            "block_digest": ("SHA-256 over the block's record digests in index order" if dblock is not None else
+                             "SHA-256 over each rank's record digests (depends on the GPU count)"),
             "blocks": {str(k): v for k, v in sorted(allb.items())},
             "global": combine_digests(allb), "rank0_blocks": sorted(mine)}
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -115,6 +115,11 @@ size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
  * intermediates, which otherwise persist until the next call.  qrk_ctx_destroy does the
  * same before freeing. */
 int qrk_ctx_cleanse(qrk_ctx *ctx);
+/* Diagnostics (tests): waits for the context's last call, then counts the nonzero bytes left
+ * in its pinned host staging (out[0]) and device staging (out[1]) -- the buffers that carry
+ * OS-drawn coins (coins == NULL) to the device, wiped before every call returns -- and in the
+ * first 64 MiB of device scratch (out[2], zero after qrk_ctx_cleanse). */
+int qrk_ctx_staging_residue(qrk_ctx *ctx, uint64_t out[3]);
 /* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
  * scratch stays near 8 GiB); 0 for an unknown algorithm. */
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);

@@ -300,6 +300,21 @@ struct TimerScope {
   ~TimerScope() { g_timer = prev; }
 };
 
+// Zeroes the pinned host and device staging copies of OS-drawn coins when run_batch returns
+// (these are the KeyGen seeds / Encaps messages, i.e. enough to rebuild the keys):
+// waits for the upload and every kernel that reads them, then wipes both, stream-ordered.
+struct CoinWipe {
+  qrk_ctx* ctx;
+  hipStream_t st;
+  size_t bytes = 0;
+  ~CoinWipe() {
+    if (!bytes) return;
+    (void)hipStreamSynchronize(st);
+    OQS_MEM_cleanse(ctx->hstage, bytes);
+    (void)hipMemsetAsync(ctx->dstage, 0, bytes, st);
+  }
+};
+
 // QRK_FIX_SIDE 1: on the single-stream schedule the ML-KEM SampleNTT fix-up kernel (about one
 // wave per SIMD, latency-bound) runs on the side stream beside the front hash and PRFs
 #ifndef QRK_FIX_SIDE
@@ -323,6 +338,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
   const size_t clen = (op == Op::KEYPAIR) ? a.kp_coins : a.enc_coins;
   bool synth = false;
+  // OS coins are KeyGen seeds / Encaps messages: wipe both staged copies on every exit path
+  // (declared after last_use, so the device wipe is queued before the call's end event)
+  CoinWipe coin_wipe{ctx, st};
   if (op != Op::DECAPS && coins == nullptr) {
     const size_t bytes = n * clen;
     if (grow_pinned(&ctx->hstage, &ctx->hstage_bytes, bytes)) return -1;
@@ -333,6 +351,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync(coins)", e);
     coins = ctx->dstage;
     synth = true;
+    coin_wipe.bytes = bytes;
   }
   if (!ctx->aux) {
     hipError_t e1 = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
@@ -348,7 +367,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   // chip and the overlap only stretches each kernel's span (profiles/r2/ab_streams*.json).
   const bool fork = ctx->streams == 2 || (ctx->streams == 0 && chunk < QRK_FORK_MAX);
   S.aux = fork ? ctx->aux : nullptr;
-  S.side = QRK_FIX_SIDE ? ctx->aux : nullptr;
+  // streams == 1 is the documented serial schedule (kernel timings in isolation, qrkem.h): no
+  // side-stream fix-up there either
+  S.side = (QRK_FIX_SIDE && ctx->streams != 1) ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
   if (ctx->flag_next) {
@@ -796,6 +817,26 @@ int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {
 }
 
 size_t qrk_ctx_scratch_bytes(const qrk_ctx* ctx) { return ctx ? ctx->scratch_bytes : 0; }
+
+int qrk_ctx_staging_residue(qrk_ctx* ctx, uint64_t out[3]) {
+  if (!ctx || !out) return fail("null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  ctx_quiesce(ctx);
+  out[0] = out[1] = out[2] = 0;
+  for (size_t i = 0; i < ctx->hstage_bytes; ++i) out[0] += ctx->hstage[i] != 0;
+  const void* src[2] = {ctx->dstage, ctx->scratch};
+  const size_t len[2] = {ctx->dstage_bytes, std::min<size_t>(ctx->scratch_bytes, (size_t)64 << 20)};
+  for (int b = 0; b < 2; ++b) {
+    if (!len[b]) continue;
+    std::vector<uint8_t> tmp(len[b]);
+    hipError_t e = hipMemcpy(tmp.data(), src[b], len[b], hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail("hipMemcpy(staging residue)", e);
+    for (uint8_t x : tmp) out[1 + b] += x != 0;
+  }
+  return 0;
+}
 
 size_t qrk_ctx_effective_chunk(const qrk_ctx* ctx, const char* alg) {
   const AlgInfo* a = find_alg(alg);

@@ -45,6 +45,7 @@ def _bind(lib: ct.CDLL) -> ct.CDLL:
         "qrk_ctx_scratch_bytes": (SZ, [P]),
         "qrk_ctx_cleanse": (ct.c_int, [P]),
         "qrk_ctx_effective_chunk": (SZ, [P, ct.c_char_p]),
+        "qrk_ctx_staging_residue": (ct.c_int, [P, ct.POINTER(ct.c_uint64)]),
         "qrk_kem_sizes": (ct.c_int, [ct.c_char_p, ct.POINTER(SZ)]),
         "qrk_kem_keypair_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P]),
         "qrk_kem_encaps_batch": (ct.c_int, [P, ct.c_char_p, SZ, P, P, P, P, P, P]),

@@ -18,9 +18,12 @@ ALG = "ML-KEM-768"
 
 
 def test_device_keypair_then_host_encaps_without_sync():
+    """m > mlkem_small_max() (1024): the host Encaps takes the batched path through the packed
+    device I/O buffer and the context scratch on the I/O stream (batches up to 1024 run on the
+    zero-copy one-launch kernels, which never touch the scratch)."""
     import oracle as orc
     from qrkem.batch import BatchKEM
-    n, m = 1 << 16, 300
+    n, m = 1 << 16, 2048
     eng = BatchKEM(ALG, device=0)
     coins = orc.bench_coins(n, 64, seed=77)
     host_kc = orc.bench_coins(m, 96, seed=78)
@@ -67,13 +70,79 @@ def test_two_device_streams_on_one_context():
     assert np.array_equal(ss0.index_select(0, ti).cpu().numpy(), oss0)
 
 
+def test_device_keypair_then_frodo_host_encaps_without_sync():
+    """FrodoKEM has no zero-copy path: even 8 host Encaps run through the context scratch, so
+    they must wait for the asynchronous device KeyGen that is still using it."""
+    import oracle as orc
+    from qrkem.batch import BatchKEM
+    fr = "FrodoKEM-640-SHAKE"
+    n, m = 1 << 12, 8
+    eng = BatchKEM(fr, device=0)
+    coins = orc.bench_coins(n, eng.kp_coins, seed=79)
+    kc = orc.bench_coins(m, eng.kp_coins, seed=80)
+    ec = np.ascontiguousarray(orc.bench_coins(m, eng.enc_coins, seed=81))
+    hpk, _ = orc.batch_keypair(fr, np.ascontiguousarray(kc))
+    dcoins = torch.from_numpy(coins).cuda()
+    torch.cuda.synchronize()
+    pk, sk = eng.keypair(coins=dcoins)          # async on the torch stream
+    ct_h, ss_h = eng.encaps(hpk, coins=ec)       # host API, own stream, same scratch
+    torch.cuda.synchronize()
+    oct_, oss = orc.batch_encaps(fr, hpk, ec)
+    assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
+    idx = np.unique(np.r_[0:2, 0:n:1021, n - 2:n])
+    opk, osk = orc.batch_keypair(fr, np.ascontiguousarray(coins[idx]))
+    ti = torch.from_numpy(idx).cuda()
+    assert np.array_equal(pk.index_select(0, ti).cpu().numpy(), opk)
+    assert np.array_equal(sk.index_select(0, ti).cpu().numpy(), osk)
+
+
+def _residue(ctx):
+    import ctypes as ct
+    from qrkem._native import LIB
+    out = (ct.c_uint64 * 3)()
+    assert LIB.qrk_ctx_staging_residue(ctx, out) == 0
+    return list(out)
+
+
+def test_os_coins_staging_wiped():
+    """coins=None draws KeyGen seeds / Encaps messages from the OS into pinned host staging and
+    uploads them to device staging; both copies are zero when the call returns."""
+    from qrkem.batch import BatchKEM
+    eng = BatchKEM(ALG, device=0)
+    pk, sk = eng.keypair(n=4096)          # batched path, OS coins
+    torch.cuda.synchronize()
+    h, d, _ = _residue(eng._ctx)
+    assert (h, d) == (0, 0)
+    ct_, ss = eng.encaps(pk)               # OS Encaps messages
+    assert bool((eng.decaps(sk, ct_) == ss).all())
+    h, d, _ = _residue(eng._ctx)
+    assert (h, d) == (0, 0)
+
+
 def test_cleanse_and_device_restore():
     """qrk_ctx_cleanse zeroes the scratch; a call leaves the caller's current device as it was."""
     from qrkem._native import LIB
     from qrkem.batch import BatchKEM
     eng = BatchKEM(ALG, device=0)
-    pk, sk = eng.keypair(n=128)
+    pk, sk = eng.keypair(n=4096)           # batched: the scratch now holds SampleNTT / PRF output
     ct_, ss = eng.encaps(pk)
     assert bool((eng.decaps(sk, ct_) == ss).all())
+    assert _residue(eng._ctx)[2] > 0
     assert LIB.qrk_ctx_cleanse(eng._ctx) == 0
+    assert _residue(eng._ctx) == [0, 0, 0]
+    assert torch.cuda.current_device() == 0
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs a second GPU")
+def test_context_on_other_device_restores_current():
+    """A context on GPU 1 used while GPU 0 is current: every call restores GPU 0 (DeviceGuard)."""
+    from qrkem.batch import BatchKEM
+    torch.cuda.set_device(0)
+    eng = BatchKEM(ALG, device=1)
+    pk, sk = eng.keypair(n=64)
+    assert torch.cuda.current_device() == 0
+    ct_, ss = eng.encaps(pk)
+    assert torch.cuda.current_device() == 0
+    assert bool((eng.decaps(sk, ct_) == ss).all())
     assert torch.cuda.current_device() == 0
