@@ -153,9 +153,9 @@ ACC = 256 * 8                      # int32 accumulator -> centered fp32 residue 
 COMPRESS = 256 * 6                 # canonicalise + Compress_d (mulhi) per coefficient
 DEC12 = 256 * 2                    # ByteDecode_12 + the FIPS 203 7.2 modulus reduction
 ENC12 = 256 * 3                    # canonicalise + ByteEncode_12
-UNPACK = 256 * 5                   # ByteDecode_d + Decompress_d per coefficient
+UNPACK = 256 * 4                   # ByteDecode_d + Decompress_d per coefficient
 PACK = 256 * 2                     # ByteEncode_d per coefficient
-DEC_MSG = 256 * 8                  # Decaps: Decompress_dv(v) - w, canonicalise, Compress_1
+DEC_MSG = 256 * 6                  # Decaps: Decompress_dv(v) - w, canonicalise, Compress_1
 
 
 def mlkem_core_ops(k, eta1, kind):

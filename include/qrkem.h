@@ -111,9 +111,12 @@ size_t qrk_ctx_scratch_bytes(const qrk_ctx *ctx);
 /* Zero every buffer of the context that can hold keys or secret intermediates (device
  * scratch, handshake scratch, device and pinned host staging); synchronous.  Every call
  * already zeroes the per-handshake key records it leaves in scratch (seeds, m', K', Kbar,
- * ...) and the staged copies of host secrets; this also clears noise-polynomial
- * intermediates, which otherwise persist until the next call.  qrk_ctx_destroy does the
- * same before freeing. */
+ * ...) and the staged copies of host secrets (coins included).  The other intermediates stay
+ * in scratch until a later call overwrites them, and some of them are expanded secret-key
+ * material: ML-KEM's PRF output for s and e (KeyGen) and for the re-encryption noise (Decaps),
+ * FrodoKEM's sampled S / S', HQC's seedexpander rows x, y (KeyGen, Decaps) and r1, r2, e.
+ * Call this (or qrk_ctx_destroy, which does the same before freeing) when a context that
+ * handled secret keys is idle. */
 int qrk_ctx_cleanse(qrk_ctx *ctx);
 /* Diagnostics (tests): waits for the context's last call, then counts the nonzero bytes left
  * in its pinned host staging (out[0]) and device staging (out[1]) -- the buffers that carry

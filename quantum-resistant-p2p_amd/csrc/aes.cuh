@@ -97,9 +97,13 @@ __device__ __forceinline__ void expand_key(const uint32_t key[4], uint32_t rk[44
 //   [0..44)  round keys rk0..rk10
 //   [44..48) C0, C3 (round-1 constants of the per-row columns), C1, C2 (per-block columns)
 //   [48 + 4 jb .. +4) uniform part of the round-2 output for column block j = 8 jb
+//   [ROWP + 4 i .. +4) per-row part of the round-2 output for row i (the column-major Gen(A) kernel,
+//                      where the column block is the lane's and the row the loop's)
 constexpr int PREP_HDR = 48;
 template <int N>
-constexpr int prep_words() { return PREP_HDR + 4 * (N / 8); }
+constexpr int prep_rowp() { return PREP_HDR + 4 * (N / 8); }
+template <int N>
+constexpr int prep_words() { return prep_rowp<N>() + 4 * N; }
 
 // ---- LDS-replicated T0 lookups.  `tl` = (lane & 31) * 4: the byte offset of this lane's
 // replica column; entry x of the table is at byte 128 x.
@@ -228,6 +232,17 @@ __device__ __forceinline__ void rounds_3_10_x2(const Lds& L, uint32_t z[4], uint
   }
   round_last(L, z, rk + 40);
   round_last(L, w, rk + 40);
+}
+
+// row_part below from the constant-memory table (the prep kernel, no LDS table): k = rk0 word 0,
+// c0 / c3 = the round-1 constants the prep header stores at [44] / [45]
+__device__ __forceinline__ void row_part_g(uint32_t k, uint32_t c0, uint32_t c3, uint32_t i, uint32_t lp[4]) {
+  const uint32_t y0 = Tg(0, (i ^ k) & 0xFF) ^ c0;
+  const uint32_t y3 = Tg(1, ((i >> 8) ^ (k >> 8)) & 0xFF) ^ c3;
+  lp[0] = Tg(0, B(y0, 0)) ^ Tg(3, B(y3, 3));
+  lp[1] = Tg(2, B(y3, 2)) ^ Tg(3, B(y0, 3));
+  lp[2] = Tg(1, B(y3, 1)) ^ Tg(2, B(y0, 2));
+  lp[3] = Tg(0, B(y3, 0)) ^ Tg(1, B(y0, 1));
 }
 
 // Per-row part of the round-2 output for row i (prep header at hp, uniform).

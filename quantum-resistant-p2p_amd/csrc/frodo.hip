@@ -406,14 +406,16 @@ __global__ __launch_bounds__(64) void k_fr_gen_mm(const uint8_t* __restrict__ se
 // Per handshake (lane per (hs, column block jb)): round keys of seedA, the round-1
 // constants and the uniform round-2 part of column block jb (aes.cuh).  seedA at
 // seed_base + hs * seed_stride (pk, or the pk copy inside sk).
-template <int N>
+// ROWS: NB + N threads per handshake, the last N of which store the per-row parts (prep_rowp) for
+// the column-major Gen(A) kernel k_fr_gen_mv_aes.
+template <int N, bool ROWS = false>
 __global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__ seed_base, size_t seed_stride,
                                                      size_t n, uint32_t* __restrict__ prep) {
   using namespace aes;
-  constexpr int NB = N / 8, W = prep_words<N>();
+  constexpr int NB = N / 8, W = prep_words<N>(), TPH = ROWS ? NB + N : NB;
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const size_t hs = t / NB;
-  const int jb = (int)(t % NB);
+  const size_t hs = t / TPH;
+  const int jb = (int)(t % TPH);
   if (hs >= n) return;
   const uint32_t* sa = (const uint32_t*)(seed_base + hs * seed_stride);
   const uint32_t key[4] = {sa[0], sa[1], sa[2], sa[3]};
@@ -426,6 +428,12 @@ __global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__
   const uint32_t C2 = Tg(0, B(r2, 0)) ^ Tg(1, B(r3, 1)) ^ Tg(3, B(r1, 3)) ^ rk[6];
   const uint32_t C3 = Tg(0, B(r3, 0)) ^ Tg(2, B(r1, 2)) ^ Tg(3, B(r2, 3)) ^ rk[7];
   uint32_t* o = prep + hs * W;
+  if (ROWS && jb >= NB) {
+    uint32_t lp[4];
+    row_part_g(rk[0], C0, C3, (uint32_t)(jb - NB), lp);
+    *(uint4*)(o + prep_rowp<N>() + 4 * (jb - NB)) = make_uint4(lp[0], lp[1], lp[2], lp[3]);
+    return;
+  }
   if (jb == 0) {
 #pragma unroll
     for (int i = 0; i < 44; ++i) o[i] = rk[i];
@@ -591,6 +599,85 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
 #endif
 }
 
+// Gen(A) with AES-128 fused with S'A on the VALU, column-major: one lane owns column block jb (8
+// columns of A) of one handshake and walks the rows i of its row range, two AES blocks in flight;
+// after round 2 a block's state is rowpart(i) ^ colpart(jb) (aes.cuh), so the lane keeps its
+// colpart in registers and reads the row parts (prep_rowp) and the S' pairs of row i
+// (S'[2q][i] | S'[2q+1][i] << 16, k_fr_kg_spairs) as it goes.  Each A value is multiplied into
+// the 8 outputs B'[k][8 jb + c] with 4 v_pk_mad_u16 (mod 2^16 is all Encaps needs: q | 2^16), so
+// the lane ends with whole sums for its columns -- no LDS staging beside the T-table (the kernel is
+// bound by the table lookups on the CU's LDS, where k_fr_gen_mm_aes's MFMA staging added ~12 %
+// more LDS instructions, while the four SIMDs have VALU to spare), and no per-wave partial sums.
+// FR_MV_R<N> row ranges per column block keep every handshake's lanes whole waves (waves never span
+// two handshakes, so round keys and S' pairs are scalar loads): 640: 80 x 4 = 320 lanes, 976: 122
+// (+ 6 idle) = 128, 1344: 168 x 8 = 1344.  Output: R partial sums [hs][R][8][N], added by k_fr_pack.
+#ifndef QRK_FR_MV_AES
+#define QRK_FR_MV_AES 1
+#endif
+template <int N>
+constexpr int fr_mv_r() { return N == 640 ? 4 : (N == 976 ? 1 : 8); }
+template <int N>
+constexpr int fr_mv_lph() { return ((N / 8) * fr_mv_r<N>() + 63) / 64 * 64; }  // lanes per handshake
+template <int N>
+__global__ __launch_bounds__(1024) void k_fr_gen_mv_aes(const uint32_t* __restrict__ prep, size_t n,
+                                                        const uint32_t* __restrict__ spair, uint16_t* __restrict__ part) {
+  using P = FP<N>;
+  constexpr int NB = N / 8, R = fr_mv_r<N>(), LPH = fr_mv_lph<N>(), RN = N / R;
+  static_assert(RN % 2 == 0, "row pairs");
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry
+  aes::fill_lds2(tab, threadIdx.x, 1024);
+  __syncthreads();
+  const size_t gl = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t hs = __builtin_amdgcn_readfirstlane((uint32_t)(gl / LPH));  // whole waves per handshake
+  const int l = (int)(gl % LPH);
+  if (hs >= n || l >= NB * R) return;
+  const int r = l / NB, jb = l % NB;
+  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
+  const uint32_t* rowp = hp + aes::prep_rowp<N>();
+  const uint32_t* sp = spair + (size_t)hs * N * 4;
+  const int lane = threadIdx.x & 63;
+  const aes::Lds2 L{(const char*)tab, (uint32_t)(lane & 31) * 4u, 128u + (uint32_t)(lane & 31) * 4u};
+  const uint4 cu = *(const uint4*)(hp + aes::PREP_HDR + 4 * jb);
+  u16x2 acc[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[c][q] = (u16x2){0, 0};
+#pragma unroll 1
+  for (int i = r * RN; i < (r + 1) * RN; i += 2) {
+    const uint4 a = *(const uint4*)(rowp + 4 * i), b = *(const uint4*)(rowp + 4 * i + 4);
+    uint32_t z[4] = {a.x ^ cu.x, a.y ^ cu.y, a.z ^ cu.z, a.w ^ cu.w};
+    uint32_t w[4] = {b.x ^ cu.x, b.y ^ cu.y, b.z ^ cu.z, b.w ^ cu.w};
+    aes::rounds_3_10_x2(L, z, w, hp);
+    const uint32_t* s0 = sp + 4 * i;  // S' pairs of rows i, i + 1 (uniform: scalar loads)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t* x = h ? w : z;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t v = x[c >> 1];
+        const u16x2 vv = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(v, v, (c & 1) ? 0x03020302u : 0x01000100u));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[c][q] = vv * __builtin_bit_cast(u16x2, s0[4 * h + q]) + acc[c][q];
+      }
+    }
+  }
+  // B'[k][8 jb + c] (partial over the row range r): 8 values per k as one 16-byte store
+  uint16_t* prt = part + ((size_t)hs * R + r) * NBAR * N + 8 * jb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t lo[4], hi[4];  // rows k = 2q (low halves) and 2q + 1 (high halves), columns c = 0..7
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t a0 = __builtin_bit_cast(uint32_t, acc[2 * e][q]), a1 = __builtin_bit_cast(uint32_t, acc[2 * e + 1][q]);
+      lo[e] = __builtin_amdgcn_perm(a1, a0, 0x05040100u);
+      hi[e] = __builtin_amdgcn_perm(a1, a0, 0x07060302u);
+    }
+    *(uint4*)(prt + (2 * q) * N) = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+    *(uint4*)(prt + (2 * q + 1) * N) = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  }
+}
+
 // LOGQ-bit MSB-first bit-field reads / writes
 template <int LOGQ>
 __device__ __forceinline__ uint32_t unpack_at(const uint8_t* p, size_t idx) {
@@ -633,7 +720,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 // MODE 0 (encaps): ct is stored with coalesced 8-byte stores, kk = k.
 // MODE 1 (decaps): ct' stays in LDS, is compared with the received ct, and
 // kk = (ct == ct') ? k' : s is selected in constant time.
-template <int N, int MODE>
+template <int N, int MODE, int NPART = FP<N>::NWV>
 __global__ __launch_bounds__(256) void k_fr_pack(size_t n, const uint8_t* __restrict__ pk_base, size_t pk_stride,
                                                  const int8_t* __restrict__ sp8, const int16_t* __restrict__ ep16,
                                                  const int16_t* __restrict__ epp16, const uint16_t* __restrict__ part,
@@ -658,7 +745,7 @@ __global__ __launch_bounds__(256) void k_fr_pack(size_t n, const uint8_t* __rest
     *(uint4*)&bsh[g * 8] = make_uint4(v[0] | (v[1] << 16), v[2] | (v[3] << 16), v[4] | (v[5] << 16), v[6] | (v[7] << 16));
   }
   // 2. B' groups: partial sums (u16 pairs, lane-wise adds) + E', masked, packed into LDS
-  const uint16_t* pp = part + hs * P::NWV * NBAR * N;
+  const uint16_t* pp = part + hs * NPART * NBAR * N;
   const int16_t* ep = ep16 + hs * NBAR * N;
   for (int g = t; g < N; g += 256) {
     uint32_t lo[4], hi[4];
@@ -669,7 +756,7 @@ __global__ __launch_bounds__(256) void k_fr_pack(size_t n, const uint8_t* __rest
       for (int q = 0; q < 4; ++q) lo[q] = e[q] & 0xFFFF, hi[q] = e[q] >> 16;
     }
 #pragma unroll 4
-    for (int w = 0; w < P::NWV; ++w) {
+    for (int w = 0; w < NPART; ++w) {
       const uint4 x = *(const uint4*)(pp + (size_t)w * NBAR * N + 8 * g);
       const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -1094,6 +1181,104 @@ __global__ __launch_bounds__(kg_threads<N>()) void k_fr_kg_rows_aes(const uint32
                  __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
 }
 
+// FrodoKEM-AES KeyGen B = A S + E (mod 2^16) with Gen(A) (AES-128, k_fr_gen_mm_aes's LDS T-table
+// and round-2 shortcut) fused with the product on i8 MFMA -- the KeyGen counterpart of the encaps
+// kernel (FrodoKEM-AES is the plugin default, key_exchange.py:319, and KeyGen runs twice
+// per exchange, messaging.py:590, 809).  One wave owns 64 consecutive rows of A (lane = row r); each
+// 16-column stage (two AES blocks) is split into balanced int8 limbs (lo = a & 0xFF, hi =
+// ((a + 128) >> 8) & 0xFF, a == 256 hi + lo mod 2^16), staged row-major, 16 bytes per row and limb
+// (one ds_write_b128 per lane), and contracted over the 16 columns:
+//   D(16 rows x 16) += X(16 rows x 32) . Y(32 x 16),  X[r][c] = limb(A[r][c0 + c]), Y[c][k] = S[c0 + c][k]
+// with v_mfma_i32_16x16x32_i8, K slices 16..31 zero (lanes 32-63 feed zero Y), four 16-row tiles x
+// two limbs = 8 MFMAs per stage, i32 accumulation over all N columns (|acc| <= N 128 12 < 2^31).
+// The VALU rows kernel spends 64 v_pk_mad_u16 per 16 columns on this product; here it is 8 byte
+// perms + 8 packed adds, 2 LDS writes, 8 LDS reads and 8 MFMAs.  A/B on one box (FrodoKEM-976-AES
+// handshake mode, profiles/r3/ab_frodo976aes_kg_mm_aes_rejected.jsonl): 69.4 ms per 2^16 KeyGen
+// against 67.5 ms for the VALU rows kernel -- the AES T-table lookups bound both kernels on the
+// CU's LDS, where the VALU multiply-adds run for free on the four SIMDs and the staging does not,
+// so 0 (the rows kernel) stays the default.
+#ifndef QRK_FR_KG_MM_AES
+#define QRK_FR_KG_MM_AES 0
+#endif
+typedef int v2i __attribute__((ext_vector_type(2)));
+template <int N>
+__global__ __launch_bounds__(64 * AES_WAVES) void k_fr_kg_mm_aes(const uint32_t* __restrict__ prep, size_t n,
+                                                                 const int8_t* __restrict__ sp8,
+                                                                 const int16_t* __restrict__ e16,
+                                                                 uint16_t* __restrict__ bmat) {
+  using P = FP<N>;
+  static_assert(N % 16 == 0, "16-column stages (AES block pairs)");
+  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry
+  __shared__ __attribute__((aligned(16))) uint8_t stb[AES_WAVES][64 * 16];  // [row][16 columns], one limb
+  aes::fill_lds2(tab, threadIdx.x, 64 * AES_WAVES);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t item = (uint32_t)blockIdx.x * AES_WAVES + (uint32_t)wave;
+  if (item >= (uint32_t)(n * P::NWV)) return;
+  const uint32_t hs = __builtin_amdgcn_readfirstlane(item / P::NWV);
+  const int wv = (int)__builtin_amdgcn_readfirstlane(item % P::NWV);
+  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
+  const aes::Lds2 L{(const char*)tab, (uint32_t)(lane & 31) * 4u, 128u + (uint32_t)(lane & 31) * 4u};
+  const int r = wv * 64 + lane;
+  const bool row_ok = r < N;
+  const int kq = lane & 15, kh = lane >> 4;  // MFMA fragment: row / column kq, K slice 8 kh .. 8 kh + 7
+  uint32_t lp[4];
+  aes::row_part(L, hp, (uint32_t)r, lp);
+  const int8_t* srow = sp8 + ((size_t)hs * NBAR + (kq & 7)) * P::NP;  // S^T row (kq & 7)
+  uint8_t* sb = stb[wave];
+  v4i acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = (v4i){0, 0, 0, 0};
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+#pragma unroll 1
+  for (int c0 = 0; c0 < N; c0 += 16) {
+    // Y: S[c0 + 8 kh .. +7][kq & 7] on K slices 0, 1; zero on slices 2, 3 (lanes 32-63)
+    v2i y = {0, 0};
+    if (kh < 2) y = *(const v2i*)(srow + c0 + 8 * kh);
+    const uint32_t* u = hp + aes::PREP_HDR + 4 * (c0 >> 3);
+    uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
+    uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
+    aes::rounds_3_10_x2(L, z, w, hp);
+    const uint32_t x[8] = {z[0], z[1], z[2], z[3], w[0], w[1], w[2], w[3]};  // values 2q, 2q + 1 in x[q]
+#pragma unroll
+    for (int limb = 0; limb < 2; ++limb) {
+      uint32_t b[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {  // bytes of values 4d .. 4d + 3
+        const uint32_t a0 = limb ? add80(x[2 * d]) : x[2 * d], a1 = limb ? add80(x[2 * d + 1]) : x[2 * d + 1];
+        b[d] = row_ok ? __builtin_amdgcn_perm(a1, a0, limb ? 0x07050301u : 0x06040200u) : 0u;
+      }
+      *(uint4*)(sb + lane * 16) = make_uint4(b[0], b[1], b[2], b[3]);
+      wsync();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const v2i xv = *(const v2i*)(sb + (16 * t + kq) * 16 + 8 * (kh & 1));
+        acc[t][limb] = __builtin_amdgcn_mfma_i32_16x16x32_i8(*(const long*)&xv, *(const long*)&y, acc[t][limb], 0, 0, 0);
+      }
+      wsync();
+    }
+  }
+  // D[m][k]: m = row 16 t + 4 (lane >> 4) + g, k = lane & 15
+  if (kq < NBAR) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int rr = wv * 64 + 16 * t + 4 * kh + g;
+        if (rr < N) {
+          const size_t o = ((size_t)hs * N + rr) * NBAR + kq;
+          const uint32_t v = (uint32_t)acc[t][0][g] + ((uint32_t)acc[t][1][g] << 8) + (uint32_t)(int)e16[o];
+          bmat[o] = (uint16_t)(v & P::QMASK);
+        }
+      }
+    }
+  }
+}
+
 // pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh.  One 256-thread workgroup
 // per handshake; packed B is staged in LDS and copied out with 8-byte stores (pkh is hashed
 // by k_fr_kg_pkh afterwards; seedA and s were written by k_fr_kg_front).
@@ -1278,11 +1463,25 @@ void launch_ss(const uint8_t* ct, size_t n, const View<N>& v, uint8_t* ss, hipSt
     QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
 }
 
+// partial sums of S'A per handshake that k_fr_pack adds: one per 64-row wave (MFMA kernels), or the
+// column-major AES kernel's row ranges
+template <int N, bool AES>
+constexpr int fr_npart() { return (AES && QRK_FR_MV_AES) ? fr_mv_r<N>() : FP<N>::NWV; }
+
 // per-wave partial sums of S'A for every handshake of the chunk (Gen(A) fused)
 template <int N, bool AES>
 void launch_sa(const View<N>& v, const uint8_t* seed_base, size_t seed_stride, size_t n, hipStream_t st) {
   using P = FP<N>;
   if constexpr (AES) {
+    if (QRK_FR_MV_AES) {
+      uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
+      QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
+      QRK_LAUNCH("k_fr_aes_prep", st, (k_fr_aes_prep<N, true>), dim3(blocks_for(n * (N / 8 + N))), dim3(256), 0, st,
+                 seed_base, seed_stride, n, v.aesp);
+      QRK_LAUNCH("k_fr_gen_mv_aes", st, k_fr_gen_mv_aes<N>, dim3(blocks_for(n * fr_mv_lph<N>(), 1024)), dim3(1024), 0,
+                 st, v.aesp, n, spair, v.part);
+      return;
+    }
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, seed_base,
                seed_stride, n, v.aesp);
     QRK_LAUNCH("k_fr_gen_mm_aes", st, k_fr_gen_mm_aes<N>, dim3(blocks_for(n * P::NWV, AES_WAVES)),
@@ -1308,7 +1507,7 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(round64(n) * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk, P::PK, n, st);
-  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
+  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 0, fr_npart<N, AES>()>), dim3((unsigned)n), dim3(256), 0, st, n, pk, (size_t)P::PK, v.sp8,
              v.ep16, v.epp16, v.part, v.seeds, mu, (size_t)P::MU, ct, nullptr, nullptr, (size_t)0, v.kk);
   launch_ss<N>(ct, n, v, ss, st);
   return hipGetLastError();
@@ -1326,7 +1525,7 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, false>), dim3(blocks_for(round64(n) * (P::SE_WORDS))), dim3(256), 0, st,
              v.raw, n, P::SE_WORDS, v.sp8, v.ep16, v.epp16);
   launch_sa<N, AES>(v, pk_in_sk, P::SK, n, st);
-  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
+  QRK_LAUNCH("k_fr_pack", st, (k_fr_pack<N, 1, fr_npart<N, AES>()>), dim3((unsigned)n), dim3(256), 0, st, n, pk_in_sk, (size_t)P::SK,
              v.sp8, v.ep16, v.epp16, v.part, v.seeds, (const uint8_t*)(v.seeds + 12), (size_t)128, nullptr, ct, sk,
              (size_t)P::SK, v.kk);
   launch_ss<N>(ct, n, v, ss, st);
@@ -1345,13 +1544,17 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(round64(n) * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
   uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
-  if (AES || !QRK_FR_KG_MM)
+  if ((AES && !QRK_FR_KG_MM_AES) || (!AES && !QRK_FR_KG_MM))
     QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
   if constexpr (AES) {
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
                (size_t)P::PK, n, v.aesp);
-    QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())), dim3(kg_threads<N>()),
-               0, st, v.aesp, n, spair, v.ep16, v.part);
+    if (QRK_FR_KG_MM_AES)
+      QRK_LAUNCH("k_fr_kg_mm_aes", st, k_fr_kg_mm_aes<N>, dim3(blocks_for(n * P::NWV, AES_WAVES)),
+                 dim3(64 * AES_WAVES), 0, st, v.aesp, n, v.sp8, v.ep16, v.part);
+    else
+      QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())),
+                 dim3(kg_threads<N>()), 0, st, v.aesp, n, spair, v.ep16, v.part);
   } else if (QRK_FR_KG_MM) {
     QRK_LAUNCH("k_fr_kg_mm", st, k_fr_kg_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, pk, n, v.sp8, v.ep16,
                v.part);

@@ -121,17 +121,32 @@ __device__ __forceinline__ int canon(int a) {
 constexpr float QF = 3329.0f;
 constexpr float QINVF = 1.0f / 3329.0f;
 constexpr float MAGIC = 12582912.0f;
+// QRK_FMAMK 1: the closing p - t q as v_fmamk_f32 (literal -q) in place of the v_fmac_f32 the
+// compiler picks, which issues at ~0.65 of the full rate (profiles/r1/valu_peak_r1b.json: fmac
+// 40.4 T, fmaak 64.4 T lane-ops/s)
+#ifndef QRK_FMAMK
+#define QRK_FMAMK 0
+#endif
+__device__ __forceinline__ float fms_q(float t, float p) {  // p - t q
+#if QRK_FMAMK
+  float r;
+  asm("v_fmamk_f32 %0, %1, 0xc5501000, %2" : "=v"(r) : "v"(t), "v"(p));
+  return r;
+#else
+  return __builtin_fmaf(t, -QF, p);
+#endif
+}
 // x mod q, centered: |result| <= 1665 for |x| < 2^24 (|x / q - rint| <= 1/2 + 3e-4)
 __device__ __forceinline__ float reduce_f(float x) {
   const float t = __builtin_fmaf(x, QINVF, MAGIC) - MAGIC;
-  return __builtin_fmaf(t, -QF, x);
+  return fms_q(t, x);
 }
 // x * z mod q, centered, exact when |x * z| < 2^24 (for |z| <= 1664: |x| < 10082):
 // the product is exact, the fma computes p - t q with a single rounding of an integer < 2^24.
 __device__ __forceinline__ float modmul_f(float x, float z) {
   const float p = x * z;
   const float t = __builtin_fmaf(p, QINVF, MAGIC) - MAGIC;
-  return __builtin_fmaf(t, -QF, p);
+  return fms_q(t, p);
 }
 __device__ __forceinline__ float i2f(int x) {  // |x| < 2^22
   return __int_as_float(0x4B400000 + x) - MAGIC;
@@ -239,6 +254,13 @@ constexpr int MAX_XOF_BLOCKS = 16;
 #ifndef QRK_XOF_TIMING_ONLY
 #define QRK_XOF_TIMING_ONLY 0
 #endif
+// QRK_TIMING_WRAP N > 0 (timing probe, wrong output, never a default build): k_xof stores and the
+// batched cores load SampleNTT entry inst at inst % N, so the sampled matrix never leaves the
+// caches (N = 4096: 2 MB) -- the step with and without Â's HBM round trip at matched work
+#ifndef QRK_TIMING_WRAP
+#define QRK_TIMING_WRAP 0
+#endif
+__host__ __device__ __forceinline__ size_t xwrap(size_t inst) { return QRK_TIMING_WRAP ? inst % QRK_TIMING_WRAP : inst; }
 // QRK_XOF_ACC 1: SampleNTT acceptance as a shifted difference (compact_block below); A/B on one
 // box no faster than v_cmp + v_cndmask (profiles/r2/ab_xof_acc_rejected.jsonl), kept as an option
 #ifndef QRK_XOF_ACC
@@ -444,7 +466,25 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, uint4* __restric
 #pragma unroll 1
   for (int b = 0; b < NB && (!ALL || cnt < 256); ++b) {
     keccak_f(s);
-#if QRK_XOF_TIMING_ONLY == 1
+#if QRK_XOF_TIMING_ONLY == 4
+    // timing probe: the permutations plus the acceptance count of every candidate (what a raw-squeeze
+    // k_xof would still have to do to build the fix-up list), no compaction, one store per block
+#pragma unroll
+    for (int t = 0; t < 14; ++t) {
+      uint32_t d[3];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int di = 3 * t + e;
+        d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
+      }
+      int c[8];
+      split12(d[0], d[1], d[2], c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cnt += c[e] < Q ? 1 : 0;
+    }
+    dst[b * TW] = make_uint4(cnt, cnt, cnt, cnt);
+    if (b == NB - 1) cnt = 256;
+#elif QRK_XOF_TIMING_ONLY == 1
     // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
     // alone, the state folded into one store per block -- wrong output, never a default build
     uint32_t f = 0;
@@ -501,7 +541,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
     KState s;
     xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
     int cnt = 0;
-    xof_blocks<false, 3, XTW>(s, cnt, out + (inst / XTW) * 32 * XTW + (inst % XTW), ring, rb);
+    xof_blocks<false, 3, XTW>(s, cnt, out + (xwrap(inst) / XTW) * 32 * XTW + (xwrap(inst) % XTW), ring, rb);
     if (cnt < 256) {
       const size_t slot = atomicAdd(nfix, 1u);
       if (slot < cap) {
@@ -1225,6 +1265,7 @@ __device__ __forceinline__ void flush_cmp(GroupLds& g, const CmpWords<D>& c, uin
 // of the producer's compacted output -- contiguous layout, no parsing.
 template <int TW = 64>
 __device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t inst, int L) {
+  if (TW == XTW) inst = xwrap(inst);
   const uint4* base = xs + (inst / TW) * 32 * TW + (inst % TW);
   const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
   return PK8{{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}};
@@ -1346,12 +1387,14 @@ __device__ unsigned long long g_ss_trace[32];
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
 template <int K, int TW = 64>
-__device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, size_t off, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
-  const size_t hs = active ? hs_raw : n - 1;
+  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see QRK_XOF_SUB)
+  const size_t hs = off + hl;                 // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
+  const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   BOp sb[K];
@@ -1375,7 +1418,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K) * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K) * Cx + hxs, L);
   CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
@@ -1387,7 +1430,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K + i + 1) * C + hss, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K + i + 1) * Cx + hxs, L);
       er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
     }
     PF16 ef;
@@ -1404,19 +1447,20 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
   }
 }
 template <int K>
-__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, size_t Cx, size_t off,
+                                                     const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
-  keygen_core_hs<K>(n, C, xof, prf, pk, sk, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+  keygen_core_hs<K>(n, C, Cx, off, xof, prf, pk, sk, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
 }
 
 // ------------------------------------------------------------ K-PKE.Encrypt core
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
 template <int K, int MODE, int TW = 64>
-__device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, size_t off, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
@@ -1425,8 +1469,10 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
-  const size_t hs = active ? hs_raw : n - 1;
+  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see QRK_XOF_SUB)
+  const size_t hs = off + hl;                 // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
+  const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
   const size_t hsm = (TW == 64 || MODE == 0) ? hs : 0;  // m', K', Kbar: LDS on the small decaps path
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
@@ -1454,7 +1500,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 #if QRK_ENC_PREFETCH
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)j * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)j * Cx + hxs, L);
 #endif
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
@@ -1467,13 +1513,13 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
 #else
 #pragma unroll
-    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(i * K + j) * C + hss, L), yb[j]);
+    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(i * K + j) * Cx + hxs, L), yb[j]);
 #endif
     const CbdRaw ecur = er;
 #if QRK_ENC_PREFETCH
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * C + hss, L);
+      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * Cx + hxs, L);
     }
 #endif
     er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
@@ -1541,7 +1587,8 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   SS_MARK(TW == 16 && L == 0, 7);
 }
 template <int K, int MODE>
-__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
+__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
+                                                      const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
@@ -1550,7 +1597,8 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
-  encrypt_core_hs<K, MODE>(n, C, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+  encrypt_core_hs<K, MODE>(n, C, Cx, off, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
+                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
 }
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
@@ -2122,6 +2170,15 @@ inline void fix_join(const Streams* fs) {
   if (fs) (void)hipStreamWaitEvent(fs->main, fs->join, 0);
 }
 
+// QRK_XOF_SUB S > 0: SampleNTT and the core that consumes it run in sub-chunks of S handshakes
+// (k_xof + fix-up + core per sub-chunk, the front hashes and PRFs over the whole chunk first), so
+// the sampled matrix of one sub-chunk (4.6 KB per ML-KEM-768 handshake) is read back from the
+// Infinity Cache instead of HBM.  0: one SampleNTT pass over the chunk.
+#ifndef QRK_XOF_SUB
+#define QRK_XOF_SUB 0
+#endif
+inline bool xof_sub(size_t n) { return QRK_XOF_SUB > 0 && n > (size_t)QRK_XOF_SUB; }
+
 template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
@@ -2134,6 +2191,21 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds);
+  if (xof_sub(n)) {
+    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
+               n, C, 2 * K, 2 * K, v.prf);
+    const size_t Cx = round64((size_t)QRK_XOF_SUB);
+    const Streams* fs = fix_side(s);
+    for (size_t off = 0; off < n; off += Cx) {
+      const size_t m = std::min(Cx, n - off);
+      launch_xof<K>(pk + off * P<K>::PK + 384 * K, (size_t)P<K>::PK, m, Cx, v, st, fs);
+      fix_join(fs);
+      QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((m + GROUPS - 1) / GROUPS)), dim3(256), 0,
+                 st, m, C, Cx, off, v.xof, v.prf, pk, sk);
+    }
+    QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
+    return hipGetLastError();
+  }
   const Streams* fs = fix_side(s);
   fork(s);
   launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
@@ -2142,7 +2214,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   join(s);
   fix_join(fs);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
-             n, C, v.xof, v.prf, pk, sk);
+             n, C, C, (size_t)0, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
@@ -2159,6 +2231,22 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const Streams* fs = fix_side(s);
+  if (xof_sub(n)) {
+    QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
+               v.seeds);
+    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+               v.seeds, n, C, 2 * K + 1, K, v.prf);
+    const size_t Cx = round64((size_t)QRK_XOF_SUB);
+    for (size_t off = 0; off < n; off += Cx) {
+      const size_t m = std::min(Cx, n - off);
+      launch_xof<K>(pk + off * P<K>::PK + 384 * K, (size_t)P<K>::PK, m, Cx, v, st, fs);
+      fix_join(fs);
+      QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
+                 dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
+                 nullptr, nullptr, nullptr);
+    }
+    return hipGetLastError();
+  }
   fork(s);
   launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
   QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
@@ -2168,8 +2256,8 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   join(s);
   fix_join(fs);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256),
-             0, st, n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
-             nullptr);
+             0, st, n, C, C, (size_t)0, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr,
+             nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -2192,6 +2280,24 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
     (void)hipStreamWaitEvent(fs->side, fs->fork, 0);
     QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
   }
+  if (xof_sub(n) && !jside) {
+    QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
+    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
+               v.seeds, v.kprime, v.kbar);
+    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+               v.seeds, n, C, 2 * K + 1, K, v.prf);
+    const size_t Cx = round64((size_t)QRK_XOF_SUB);
+    for (size_t off = 0; off < n; off += Cx) {
+      const size_t m = std::min(Cx, n - off);
+      launch_xof<K>(sk + off * P<K>::SK + 768 * K, (size_t)P<K>::SK, m, Cx, v, st, fs);
+      fix_join(fs);
+      QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
+                 dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK,
+                 (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, v.kprime, v.kbar,
+                 ss);
+    }
+    return hipGetLastError();
+  }
   fork(s);
   launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd, fs);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
@@ -2205,7 +2311,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
              v.seeds, n, C, 2 * K + 1, K, v.prf);
   join(s);
   fix_join(fs);
-  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, v.xof, v.prf,
+  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, C, (size_t)0, v.xof, v.prf,
              sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
              (int32_t*)nullptr, v.kprime, v.kbar, ss);
   return hipGetLastError();

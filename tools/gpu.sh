@@ -71,7 +71,7 @@ ab() {
   local tags=()
   while [ $# -gt 0 ] && [ "$1" != "--" ]; do tags+=("$1"); shift; done
   [ $# -gt 0 ] && shift
-  local f=$O/ab_$(echo "${tags[*]}" | tr ' /:' '_--').jsonl
+  local f=$O/ab_$(echo "${tags[*]}" | sed 's#[ /:]#_#g').jsonl
   for r in $(seq 1 "$rounds"); do
     for t in "${tags[@]}"; do
       _ab_one "$t" "$@" >> "$f" || { echo "ab $t failed"; return 1; }
