@@ -634,7 +634,8 @@ struct P {
 // KeyGen front: (rho, sigma) = G(d || k).  rho -> pk[384k..] and dk's ek copy; sigma -> seeds.
 template <int K>
 __device__ __forceinline__ void front_keygen_hs(const uint8_t* __restrict__ coins, size_t hs, uint8_t* __restrict__ pk,
-                                                uint8_t* __restrict__ sk, uint64_t* __restrict__ seeds) {
+                                                uint8_t* __restrict__ sk, uint64_t* __restrict__ seeds,
+                                                uint64_t* __restrict__ rho) {
   const uint64_t* d = (const uint64_t*)(coins + hs * 64);
   KState s;
   kzero(s);
@@ -650,14 +651,15 @@ __device__ __forceinline__ void front_keygen_hs(const uint8_t* __restrict__ coin
     rho_pk[w] = kword(s, w);
     rho_sk[w] = kword(s, w);
     seeds[hs * 4 + w] = kword(s, 4 + w);
+    if (rho) rho[hs * 4 + w] = kword(s, w);
   }
 }
 template <int K>
 __global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict__ coins, size_t n,
                                                       uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
-                                                      uint64_t* __restrict__ seeds) {
+                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ rho) {
   const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs < n) front_keygen_hs<K>(coins, hs, pk, sk, seeds);
+  if (hs < n) front_keygen_hs<K>(coins, hs, pk, sk, seeds, rho);
 }
 
 // KeyGen back: dk = dk_pke || ek || H(ek) || z  (ek already copied by the core kernel)
@@ -1331,10 +1333,11 @@ struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
   uint32_t* fixrec;      // SampleNTT resume records (QRK_XOF_RESUME)
+  uint64_t* rho;         // QRK_RHO_COMPACT: every handshake's rho, 32 B apart
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
   return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 2 +
-         xof_rec_cap(K, C) * XOF_REC_WORDS / 2;
+         xof_rec_cap(K, C) * XOF_REC_WORDS / 2 + 4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -1355,7 +1358,24 @@ inline ScratchView carve(void* base, int K, size_t C) {
   v.fix = v.nfix + 2;
   p += ((size_t)K * K * C + 2) / 2 + 2;
   v.fixrec = (uint32_t*)p;
+  p += xof_rec_cap(K, C) * XOF_REC_WORDS / 2;
+  v.rho = p;
   return v;
+}
+
+// QRK_RHO_COMPACT 1: k_xof reads rho from a compact copy (32 B per handshake) instead of the
+// keys themselves.  Its K^2 lanes per handshake sit in K^2 different waves, and each wave's 64
+// rho reads at the key stride (1184 B for ML-KEM-768) touch 64 cache lines: rocprofv3 counts
+// 1.2 GB of reads per 2^20-handshake k_xof launch for 33 MB of rho
+// (profiles/r3/rocprof_mlkem768_b20_r3b.json).  The copy is one 32-B read per handshake.
+#ifndef QRK_RHO_COMPACT
+#define QRK_RHO_COMPACT 1
+#endif
+__global__ __launch_bounds__(256) void k_rho_copy(const uint8_t* __restrict__ base, size_t stride, size_t n,
+                                                  uint64_t* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;  // one thread per word
+  if (t >= 4 * n) return;
+  out[t] = ((const uint64_t*)(base + (t >> 2) * stride))[t & 3];
 }
 
 // ------------------------------------------------------------ single-shot phase trace (tools only)
@@ -2179,6 +2199,21 @@ inline void fix_join(const Streams* fs) {
 #endif
 inline bool xof_sub(size_t n) { return QRK_XOF_SUB > 0 && n > (size_t)QRK_XOF_SUB; }
 
+// Where k_xof reads rho: the compact copy (copied here from the keys unless `copy` is false, i.e.
+// KeyGen's front kernel wrote it), or the keys themselves.
+struct RhoSrc {
+  const uint8_t* base;
+  size_t stride;
+  const uint8_t* at(size_t off) const { return base + off * stride; }
+};
+inline RhoSrc rho_src(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st,
+                      bool copy) {
+  if (!QRK_RHO_COMPACT) return {keys_rho, key_stride};
+  if (copy)
+    QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho);
+  return {(const uint8_t*)v.rho, (size_t)32};
+}
+
 template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
@@ -2190,7 +2225,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
-             v.seeds);
+             v.seeds, QRK_RHO_COMPACT ? v.rho : nullptr);
+  const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, false);
   if (xof_sub(n)) {
     QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
                n, C, 2 * K, 2 * K, v.prf);
@@ -2198,7 +2234,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
     const Streams* fs = fix_side(s);
     for (size_t off = 0; off < n; off += Cx) {
       const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(pk + off * P<K>::PK + 384 * K, (size_t)P<K>::PK, m, Cx, v, st, fs);
+      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
       fix_join(fs);
       QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((m + GROUPS - 1) / GROUPS)), dim3(256), 0,
                  st, m, C, Cx, off, v.xof, v.prf, pk, sk);
@@ -2208,7 +2244,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   }
   const Streams* fs = fix_side(s);
   fork(s);
-  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
+  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
              n, C, 2 * K, 2 * K, v.prf);
   join(s);
@@ -2232,6 +2268,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const Streams* fs = fix_side(s);
   if (xof_sub(n)) {
+    const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, true);
     QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
                v.seeds);
     QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
@@ -2239,7 +2276,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
     const size_t Cx = round64((size_t)QRK_XOF_SUB);
     for (size_t off = 0; off < n; off += Cx) {
       const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(pk + off * P<K>::PK + 384 * K, (size_t)P<K>::PK, m, Cx, v, st, fs);
+      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
       fix_join(fs);
       QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
                  dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
@@ -2248,7 +2285,8 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
     return hipGetLastError();
   }
   fork(s);
-  launch_xof<K>(pk + 384 * K, (size_t)P<K>::PK, n, C, v, sd, fs);
+  const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, sd, true);
+  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
   QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
              v.seeds);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
@@ -2281,6 +2319,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
     QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
   }
   if (xof_sub(n) && !jside) {
+    const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, st, true);
     QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
     QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
                v.seeds, v.kprime, v.kbar);
@@ -2289,7 +2328,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
     const size_t Cx = round64((size_t)QRK_XOF_SUB);
     for (size_t off = 0; off < n; off += Cx) {
       const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(sk + off * P<K>::SK + 768 * K, (size_t)P<K>::SK, m, Cx, v, st, fs);
+      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
       fix_join(fs);
       QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
                  dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK,
@@ -2299,7 +2338,8 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
     return hipGetLastError();
   }
   fork(s);
-  launch_xof<K>(sk + 768 * K, (size_t)P<K>::SK, n, C, v, sd, fs);
+  const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, sd, true);
+  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
   if (jside)
     QRK_LAUNCH("k_g_decaps", st, k_g_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, sk, v.mprime, n, v.seeds,
