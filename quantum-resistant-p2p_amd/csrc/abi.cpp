@@ -138,6 +138,7 @@ struct qrk_ctx {
   uint8_t* hio_dev = nullptr;     // device mapping of hio (zero-copy small calls)
   uint32_t* hflag = nullptr;      // single-shot completion flag (fine-grained pinned) ...
   uint32_t* hflag_dev = nullptr;  // ... its device address
+  uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
   hipStream_t io_stream = nullptr;
@@ -375,6 +376,14 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
+  }
+  if (a.family == Family::MLKEM && op == Op::KEYPAIR && n <= mlkem_kg_multi_max()) {
+    if (!ctx->kg_cnt) {
+      hipError_t e = hipMalloc((void**)&ctx->kg_cnt, mlkem_kg_multi_max() * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipMemset(ctx->kg_cnt, 0, mlkem_kg_multi_max() * sizeof(uint32_t));
+      if (e != hipSuccess) return hip_fail("hipMalloc(kg_cnt)", e);
+    }
+    S.kg_cnt = ctx->kg_cnt;
   }
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   for (size_t off = 0; off < n; off += chunk) {
@@ -796,6 +805,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->io_stream) (void)hipStreamDestroy(ctx->io_stream);
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
+  if (ctx->kg_cnt) (void)hipFree(ctx->kg_cnt);
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);

@@ -621,7 +621,6 @@ constexpr int fr_mv_lph() { return ((N / 8) * fr_mv_r<N>() + 63) / 64 * 64; }  /
 template <int N>
 __global__ __launch_bounds__(1024) void k_fr_gen_mv_aes(const uint32_t* __restrict__ prep, size_t n,
                                                         const uint32_t* __restrict__ spair, uint16_t* __restrict__ part) {
-  using P = FP<N>;
   constexpr int NB = N / 8, R = fr_mv_r<N>(), LPH = fr_mv_lph<N>(), RN = N / R;
   static_assert(RN % 2 == 0, "row pairs");
   __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry

@@ -839,7 +839,6 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
   constexpr int PC = P::TPB / NBT;
   const int tt = hq_tid();
   const int j0 = (tt % NBT) * WPT;
-  const bool lane63 = (tt & 63) == 63;
   // one operand: unrolled so the next position's support read and window are in flight together;
   // two operands: not unrolled (both windows already in flight; keeps <= 64 VGPRs, 8 waves / SIMD)
   constexpr int UNR = NV == 1 ? 2 : 1;

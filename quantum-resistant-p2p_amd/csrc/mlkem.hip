@@ -2135,6 +2135,153 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
   wipe_one(sl, done, ticket);
 }
 
+// ------------------------------------------------------------ single-shot KeyGen over K^2 + 2K workgroups
+// k_keygen_one runs the 2K PRFs and K^2 SampleNTT entries of one handshake as 15 waves (ML-KEM-768)
+// of one workgroup: their cooperative permutations share one CU and take ~2x their isolated time
+// (phase trace: 18.8 us for 3 + 1 sequential permutations, profiles/r2/single_shot_trace_final.json).
+// For n <= QRK_KG_MULTI_MAX the items get a one-wave workgroup each, on different CUs: every
+// workgroup runs G(d || k) itself (one permutation, no cross-workgroup wait), then its item, writes
+// the result to the context scratch (MkScr) and counts itself in with a device-scope fence and an
+// atomic add; the workgroup that arrives last computes t_hat on four 16-lane groups, hashes ek
+// (H(ek), 9 permutations at ML-KEM-768) and wipes the scratch and its counter.  No workgroup waits
+// for another (the last one simply finds everything published), so nothing can spin.
+#ifndef QRK_KG_MULTI_MAX
+#define QRK_KG_MULTI_MAX 16
+#endif
+struct MkScr {
+  uint4 xs[32 * 16];        // SampleNTT entries, load_sampled<16> layout (K^2 <= 16)
+  uint32_t bop[4][16][16];  // NTT(s_j) basemul operands, word w of lane L at [j][w][L]
+  float ef[4][16][16];      // NTT(e_i), coefficient t of lane L at [i][t][L]
+};
+struct MkLds {
+  uint64_t ps[PRF_W * 16];
+  uint32_t pbuf[44];
+  uint64_t rho[4], sigma[4];
+  uint64_t io[200];  // ek (KeyGen's LDS copy for H(ek)): 1568 B at K = 4
+  GroupLds g[4];
+  int last;
+};
+__device__ __forceinline__ void mk_wipe_lds(MkLds& sl) {
+  __syncthreads();
+  uint4* w = (uint4*)&sl;
+  for (int x = threadIdx.x; x < (int)(sizeof(MkLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
+}
+
+template <int K>
+__global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __restrict__ coins,
+                                                     uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                     MkScr* __restrict__ scr_all, uint32_t* __restrict__ cnt,
+                                                     uint32_t* done, uint32_t ticket) {
+  constexpr int NI = 2 * K + K * K;
+  __shared__ __attribute__((aligned(16))) MkLds sl;
+  const size_t hs = blockIdx.x / NI;
+  const int item = (int)(blockIdx.x % NI);
+  const int lane = threadIdx.x;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  MkScr& scr = scr_all[hs];
+  uint8_t* ek = pk + hs * P<K>::PK;
+  uint8_t* dk = sk + hs * P<K>::SK;
+  {  // (rho, sigma) = G(d || k), in every workgroup
+    const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+    CState g;
+    if (i >= 0 && i < 4) cs_xor(g, d[i]);
+    if (i == 4) g.lo ^= (uint32_t)K | (DS_SHA3 << 8);
+    if (i == RW_SHA3_512 - 1) g.hi ^= 0x80000000u;
+    g = kf_coop(g, c);
+    if (i >= 0 && i < 4 && coop_canon(c)) sl.rho[i] = cs_word(g);
+    if (i >= 4 && i < 8 && coop_canon(c)) sl.sigma[i - 4] = cs_word(g);
+    wave_phase();
+  }
+  if (item < 2 * K) {  // PRF(sigma, item) -> CBD -> NTT: s_item (operand + dk) or e_(item - K)
+    prf_coop<P<K>::ETA1>(sl.sigma, item, sl.ps, c);
+    wave_phase();
+    if (lane < 16) {
+      PF16 f;
+      cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1, 16>(sl.ps, (size_t)item, lane));
+      contig_to_stride_f(f, (float*)sl.g[0].poly, lane);
+      ntt_fwd_f<false>(f, (float*)sl.g[0].poly, lane);
+      if (item < K) {
+        const BOp b = make_bop_f(f, lane);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          scr.bop[item][u][lane] = b.b0[u];
+          scr.bop[item][8 + u][lane] = b.b1[u];
+        }
+        P16 t;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
+        encode12(t, dk + 384 * item, lane);
+      } else {
+#pragma unroll
+        for (int x = 0; x < 16; ++x) scr.ef[item - K][x][lane] = f.v[x];
+      }
+    }
+  } else {  // SampleNTT entry e = x K + y straight into the scratch
+    xof_coop<K>(sl.rho, item - 2 * K, (uint16_t*)scr.xs, sl.pbuf, c);
+  }
+  // publish, then count in: the last of the NI workgroups of this handshake finishes it
+  __threadfence();
+  __syncthreads();
+  if (lane == 0) sl.last = (int)(atomicAdd(&cnt[hs], 1u) == (uint32_t)(NI - 1));
+  __syncthreads();
+  if (!sl.last) {
+    mk_wipe_lds(sl);
+    return;
+  }
+  __threadfence();  // acquire: the other workgroups' stores are visible past the counter
+  if ((lane >> 4) < K) {  // t_hat_r = sum_j A[r][j] o s_hat_j + e_hat_r, one 16-lane group per row
+    const int r = lane >> 4, L = lane & 15;
+    int acc[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t] = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      BOp b;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        b.b0[u] = scr.bop[j][u][L];
+        b.b1[u] = scr.bop[j][8 + u][L];
+      }
+      basemul_acc(acc, load_sampled<16>(scr.xs, (size_t)(j * K + r), L), b);
+    }
+    P16 t;
+#pragma unroll
+    for (int x = 0; x < 16; ++x) t.v[x] = canon_f(acc_to_f(acc[x]) + scr.ef[r][x][L]);
+    encode12(t, ek + 384 * r, L);
+    encode12(t, dk + 384 * K + 384 * r, L);
+    encode12(t, (uint8_t*)sl.io + 384 * r, L);
+  }
+  if (lane < 4) {
+    ((uint64_t*)(ek + 384 * K))[lane] = sl.rho[lane];
+    ((uint64_t*)(dk + 768 * K))[lane] = sl.rho[lane];
+    sl.io[48 * K + lane] = sl.rho[lane];
+  }
+  wave_phase();
+  {  // dk tail: H(ek) || z
+    CState s;
+    coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return sl.io[w]; });
+    uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
+    const uint64_t* z = (const uint64_t*)(coins + hs * 64 + 32);
+    if (i >= 0 && i < 4 && coop_canon(c)) {
+      tail[i] = cs_word(s);
+      tail[4 + i] = z[i];
+    }
+  }
+  // wipe the handshake's scratch (s_hat, e_hat, A) and reset its counter for the next call
+  {
+    uint4* w = (uint4*)&scr;
+    for (int x = lane; x < (int)(sizeof(MkScr) / 16); x += 64) w[x] = make_uint4(0, 0, 0, 0);
+  }
+  if (lane == 0) atomicSub(&cnt[hs], (uint32_t)NI);
+  if (done) __threadfence_system();
+  mk_wipe_lds(sl);
+  if (done && lane == 0) {
+    // n == 1: the only handshake; the flag means every output is visible to the host
+    __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ============================================================ host launchers
 
 inline unsigned blocks_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
@@ -2218,6 +2365,11 @@ template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
+  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
+    QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
+               s.main, n, coins, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
+    return hipGetLastError();
+  }
   if (n <= QRK_SMALL_MAX) {
     QRK_LAUNCH("k_keygen_one", s.main, k_keygen_one<K>, dim3((unsigned)n), dim3(64 * KG_WAVES), 0, s.main, n, coins,
                pk, sk, n == 1 ? s.done : nullptr, s.ticket);
@@ -2360,10 +2512,12 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
 }  // namespace mlkem
 
 size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
-  return mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8;
+  // the multi-workgroup KeyGen keeps one MkScr per handshake in the scratch
+  return std::max(mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8, mlkem::round64(chunk) * sizeof(mlkem::MkScr));
 }
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
+size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }
 
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
   // the one-launch kernels (n <= QRK_SMALL_MAX) keep their key material in LDS and wipe it

@@ -57,6 +57,8 @@ size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 // ML-KEM batches up to this size run as one launch per operation with no scratch key material
 size_t mlkem_small_max();
+// ML-KEM KeyGen batches up to this size run one workgroup per SampleNTT / PRF item (latency)
+size_t mlkem_kg_multi_max();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 
@@ -73,6 +75,9 @@ struct Streams {
   // kernels store `ticket` there once their outputs are visible to the host
   uint32_t* done = nullptr;
   uint32_t ticket = 0;
+  // per-handshake arrival counters of the multi-workgroup single-shot ML-KEM KeyGen (device,
+  // QRK_KG_MULTI_MAX words, zero between calls: the last workgroup of a handshake resets its word)
+  uint32_t* kg_cnt = nullptr;
 };
 
 // All pointers are device pointers; n handshakes processed as one chunk

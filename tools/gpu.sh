@@ -21,6 +21,8 @@
 #   sq <tag> [args]           two SQ counter passes (instruction mix, stalls, LDS)
 #   mfma <tag> [args]         int8 MFMA counter pass
 #   probe <name> <hip> [flags]  build tools/<hip> with hipcc and run it -> <name>.txt
+#   pmcbin <name> <binary> <counter...>   one --pmc pass over a prebuilt probe binary
+#   run <tag> <command...>    any other GPU command -> <tag>.txt
 # Every GPU step runs under its own timeout; a failing step returns non-zero.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/misc
@@ -143,5 +145,14 @@ pmcbin() {
     timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$O/$name" -o run -- "$R/$bin" > "$O/$name.out" 2> "$O/$name.err" )
   local rc=$?
   echo "pmcbin $name rc=$rc"
+  return $rc
+}
+
+# run <tag> <command...>: any GPU command under a 300 s limit, stdout+stderr -> <tag>.txt
+run() {
+  local tag=$1; shift
+  timeout -k 10 ${RUN_TIMEOUT:-300} "$@" > "$O/$tag.txt" 2>&1
+  local rc=$?
+  echo "run $tag rc=$rc"
   return $rc
 }
