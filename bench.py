@@ -952,7 +952,10 @@ def main():
             mfma["counters"] = pmc_mfma(alg, args.mode, chunk_eff, mfma["kernel"].split()[0])
         tb, src = pmc_traffic(alg, args.mode, chunk_eff, roof["kernel"])
         roof["traffic"] = tb
-        roof["traffic_unit"] = "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)"
+        roof["traffic_unit"] = ("HBM bytes per launch: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE; the x 2 is calibrated on "
+                                "this library's own read patterns (0.500 for every coalesced width, 4-16 B/lane and the "
+                                "cores' 64-B runs; 0.774 for lane-per-record AoS reads, i.e. real over-fetch) and "
+                                "WRITE_SIZE reads exact (profiles/r3/fetch_calibration.json)")
         roof["traffic_source"] = src
         roof["algorithmic_ops_per_launch"] = roof.pop("ops_per_launch")
         roof["isolated_frac"] = roof_iso["frac"] if roof_iso and roof_iso["kernel"] == roof["kernel"] else None

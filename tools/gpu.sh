@@ -23,6 +23,7 @@
 #   probe <name> <hip> [flags]  build tools/<hip> with hipcc and run it -> <name>.txt
 #   pmcbin <name> <binary> <counter...>   one --pmc pass over a prebuilt probe binary
 #   run <tag> <command...>    any other GPU command -> <tag>.txt
+#   sweep                     one bench line per BASELINE config and SURVEY 8f mode
 # Every GPU step runs under its own timeout; a failing step returns non-zero.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/misc
@@ -155,4 +156,21 @@ run() {
   local rc=$?
   echo "run $tag rc=$rc"
   return $rc
+}
+
+# sweep: one bench line (CPU baseline included) for every BASELINE.json config and SURVEY 8f mode
+sweep() {
+  bench mlkem768 && bench mlkem512 --alg ML-KEM-512 && bench mlkem1024 --alg ML-KEM-1024 &&
+  bench mlkem1024_tampered --alg ML-KEM-1024 --mode decaps-tampered &&
+  bench mlkem768_2p24 --global-log2-batch 24 --steps 3 --warmup 1 &&
+  bench frodo640 --alg FrodoKEM-640-SHAKE && bench frodo976 --alg FrodoKEM-976-SHAKE &&
+  bench frodo1344 --alg FrodoKEM-1344-SHAKE --steps 3 --warmup 1 &&
+  bench frodo640aes --alg FrodoKEM-640-AES && bench frodo976aes --alg FrodoKEM-976-AES &&
+  bench frodo1344aes --alg FrodoKEM-1344-AES --steps 3 --warmup 1 &&
+  bench hqc128 --alg HQC-128 && bench hqc192 --alg HQC-192 && bench hqc256 --alg HQC-256 &&
+  bench hqc128_tampered --alg HQC-128 --mode decaps-tampered &&
+  bench handshake_mlkem768 --mode handshake &&
+  bench handshake_frodo976aes --alg FrodoKEM-976-AES --mode handshake --steps 3 --warmup 1 &&
+  bench handshake_hqc128 --alg HQC-128 --mode handshake &&
+  bench wire_mlkem768 --mode wire
 }
