@@ -21,6 +21,7 @@
 // (word w of instance i at ((i/64)*W + w)*64 + i%64): every lane-per-instance
 // store is a fully coalesced 512-byte wave store.
 #include <algorithm>
+#include <type_traits>
 
 #include "keccak.cuh"
 #include "keccak_coop.cuh"
@@ -71,22 +72,27 @@ constexpr Tables make_tables() {
 constexpr Tables TABC = make_tables();          // compile-time indexed twiddles
 __constant__ Tables TABD = make_tables();       // lane-indexed twiddles
 
-// Plain-domain twiddles as fp32 (centered integers, exact): the NTTs run in fp32.
+// Plain-domain twiddles as fp32 (centered integers, exact): the NTTs run in fp32.  zq is z
+// divided by q (rounded to fp32) for the three-FMA modular product below.
 struct TablesF {
   float z[128];  // zeta^br7(i) mod q
   float g[128];  // gamma_i = zeta^(2 br7(i) + 1) mod q
+  float zq[128];
 };
 constexpr TablesF make_tables_f() {
   TablesF t{};
   for (int i = 0; i < 128; ++i) {
     t.z[i] = (float)centered(powq(17, br7(i)));
     t.g[i] = (float)centered(powq(17, 2 * br7(i) + 1));
+    t.zq[i] = (float)((double)t.z[i] / 3329.0);
   }
   return t;
 }
 constexpr TablesF TABFC = make_tables_f();
 __constant__ TablesF TABFD = make_tables_f();
-constexpr float INV128F = (float)centered(3303);  // 128^-1 mod q (plain domain)
+constexpr float INV128F = (float)centered(3303);  // 128^-1 mod q (plain domain) = -26
+// zeta_1 * 128^-1: the inverse NTT's last layer folds the 128^-1 scaling into its twiddle
+constexpr float Z1INV128F = (float)centered((long)powq(17, br7(1)) * 3303);
 
 // ---------------------------------------------------------------- arithmetic
 // x < 0 ? -1 : 0 as one v_ashrrev_i32 (inline asm, so the compiler keeps the mask arithmetic
@@ -136,14 +142,47 @@ __device__ __forceinline__ float fms_q(float t, float p) {  // p - t q
   return __builtin_fmaf(t, -QF, p);
 #endif
 }
+// QRK_MODMUL3 1: the modular product / reduction as three FMAs with MAGIC folded into the
+// constants (below); 0: the round-2 form (product, rounding FMA, MAGIC subtraction, FMA).
+#ifndef QRK_MODMUL3
+#define QRK_MODMUL3 1
+#endif
+// MAGIC * q = 9987 * 2^22, exact in fp32
+constexpr float MQF = MAGIC * QF;
 // x mod q, centered: |result| <= 1665 for |x| < 2^24 (|x / q - rint| <= 1/2 + 3e-4)
+// Three-FMA form: k = x/q + MAGIC rounds to MAGIC + kint (the binade [2^23, 2^24) has ulp 1);
+// fma(k, -q, MAGIC q) = -q kint exactly (|q kint| < 2^24 for |x| <= 1.677e7); x + that is exact.
 __device__ __forceinline__ float reduce_f(float x) {
+#if QRK_MODMUL3
+  const float k = __builtin_fmaf(x, QINVF, MAGIC);
+  return x + __builtin_fmaf(k, -QF, MQF);
+#else
   const float t = __builtin_fmaf(x, QINVF, MAGIC) - MAGIC;
   return fms_q(t, x);
+#endif
 }
-// x * z mod q, centered, exact when |x * z| < 2^24 (for |z| <= 1664: |x| < 10082):
-// the product is exact, the fma computes p - t q with a single rounding of an integer < 2^24.
-__device__ __forceinline__ float modmul_f(float x, float z) {
+// x * z mod q, centered, exact when |x * z| < 2^24 (for |z| <= 1664: |x| < 10082).
+// zq = fl(z / q).  Three FMAs: k = MAGIC + round(x zq) (|x zq - x z / q| < 3e-4, so the
+// result stays within q/2 + 1), n = -q round(.) exactly, then x z + n with one rounding of an
+// exact integer below 2^24.  The round-2 form (QRK_MODMUL3 0) spent a product, the MAGIC
+// subtraction and a three-VGPR fmac (0.65 of the full rate, profiles/r1/valu_peak_r1b.json).
+__device__ __forceinline__ float modmul_f(float x, float z, float zq) {
+#if QRK_MODMUL3
+  const float k = __builtin_fmaf(x, zq, MAGIC);
+  return __builtin_fmaf(x, z, __builtin_fmaf(k, -QF, MQF));
+#else
+  (void)zq;
+  const float p = x * z;
+  const float t = __builtin_fmaf(p, QINVF, MAGIC) - MAGIC;
+  return fms_q(t, p);
+#endif
+}
+// The same product for lane-indexed twiddles (the NTT layers after the transpose, basemul gamma)
+// stays on the round-2 form: its single constant per twiddle holds fewer live registers than z
+// and z / q together.  The three-FMA form there (z / q from a table or from z * (1/q)) cost the
+// encrypt core a wave per SIMD (170 VGPRs: 2.64 against 2.29 ms per 2^20 launch) and the decrypt
+// core one too (106 against 91 VGPRs: 0.95 against 0.90 ms), profiles/r3/ab_core_arith_*.jsonl.
+__device__ __forceinline__ float modmul_lf(float x, float z) {
   const float p = x * z;
   const float t = __builtin_fmaf(p, QINVF, MAGIC) - MAGIC;
   return fms_q(t, p);
@@ -168,8 +207,20 @@ __device__ __forceinline__ int canon_f(float x) {
 }
 // basemul accumulator (|acc| < 2^31) -> centered residue: acc = hi 2^16 + lo with
 // 2^16 = -1044 (mod q), |hi * 1044 + lo| < 5.1e6 (exact), then one reduction
+// QRK_ACC2 1: with HI = MAGIC + hi and LO = MAGIC + lo as bit patterns (no MAGIC subtractions),
+// fma(HI, -1044, 1043 MAGIC) = -MAGIC - 1044 hi is an exact integer below 2^24 (|hi| < 2^11) and
+// adding LO leaves lo - 1044 hi exactly: two full-rate ops where the round-2 form spent two
+// subtractions and a three-VGPR fmac.
+#ifndef QRK_ACC2
+#define QRK_ACC2 1
+#endif
 __device__ __forceinline__ float acc_to_f(int acc) {
+#if QRK_ACC2
+  const float hi = __int_as_float(0x4B400000 + (acc >> 16)), lo = __int_as_float(0x4B400000 | (acc & 0xFFFF));
+  return reduce_f(__builtin_fmaf(hi, -1044.0f, 1043.0f * MAGIC) + lo);
+#else
   return reduce_f(__builtin_fmaf(i2f(acc >> 16), -1044.0f, i2f(acc & 0xFFFF)));
+#endif
 }
 
 // Compress_d(x) = round(2^d x / q) mod 2^d for x in [0, q): exact via 24-bit mulhi
@@ -268,6 +319,16 @@ __host__ __device__ __forceinline__ size_t xwrap(size_t inst) { return QRK_TIMIN
 #endif
 #ifndef QRK_ENC_PREFETCH
 #define QRK_ENC_PREFETCH 1
+#endif
+// QRK_EK_PREFETCH 1: the encrypt core loads t_hat (for v) during the last u-row into the
+// matrix prefetch registers, instead of when v's basemul needs it (SQ: the core waits on memory
+// 25-29 % of its wave time, profiles/r2/sq_mlkem768_b20_r2b.txt)
+#ifndef QRK_EK_PREFETCH
+#define QRK_EK_PREFETCH 1
+#endif
+// QRK_DK_PREFETCH 1: the decrypt core issues s_hat_j's load before u_j's NTT
+#ifndef QRK_DK_PREFETCH
+#define QRK_DK_PREFETCH 1
 #endif
 #define QRK_XOF_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_XOF)))
 #define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
@@ -951,7 +1012,8 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       if (((m / step) & 1) == 0) {
-        const float t = modmul_f(p.v[m + step], TABFC.z[(1 << lg) + m / (2 * step)]);
+        const int zi = (1 << lg) + m / (2 * step);
+        const float t = modmul_f(p.v[m + step], TABFC.z[zi], TABFC.zq[zi]);
         p.v[m + step] = p.v[m] - t;
         p.v[m] = p.v[m] + t;
       }
@@ -966,7 +1028,7 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
     const float z = TABFD.z[16 + L];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const float u = modmul_f(p.v[t + 8], z);
+      const float u = modmul_lf(p.v[t + 8], z);
       p.v[t + 8] = p.v[t] - u;
       p.v[t] = p.v[t] + u;
     }
@@ -976,7 +1038,7 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       if (((t >> 2) & 1) == 0) {
-        const float u = modmul_f(p.v[t + 4], t < 8 ? z0 : z1);
+        const float u = modmul_lf(p.v[t + 4], t < 8 ? z0 : z1);
         p.v[t + 4] = p.v[t] - u;
         p.v[t] = p.v[t] + u;
       }
@@ -989,7 +1051,7 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       if (((t >> 1) & 1) == 0) {
-        const float u = modmul_f(p.v[t + 2], z[t >> 2]);
+        const float u = modmul_lf(p.v[t + 2], z[t >> 2]);
         p.v[t + 2] = p.v[t] - u;
         p.v[t] = p.v[t] + u;
       }
@@ -999,7 +1061,12 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
 
 // FIPS 203 Alg. 10 in fp32 (including the 128^-1 scaling).  In: contiguous, |f| <= 1665.
 // Out: stride layout, |f| <= 1665.  Gentleman-Sande sums double per layer; the sums of
-// every second layer are reduced, so |y - x| <= 6660 at every twiddle product.
+// every second layer are reduced, so |y - x| <= 6660 at every twiddle product.  The last
+// layer folds the scaling in (QRK_INV_FOLD): x + y times 128^-1 = -26 and y - x times
+// zeta_1 128^-1, instead of a separate product for all 16 outputs.
+#ifndef QRK_INV_FOLD
+#define QRK_INV_FOLD 1
+#endif
 __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
   {
     float z[4];
@@ -1010,7 +1077,7 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
       if (((t >> 1) & 1) == 0) {
         const float x = p.v[t], y = p.v[t + 2];
         p.v[t] = x + y;
-        p.v[t + 2] = modmul_f(y - x, z[t >> 2]);
+        p.v[t + 2] = modmul_lf(y - x, z[t >> 2]);
       }
     }
   }
@@ -1021,7 +1088,7 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
       if (((t >> 2) & 1) == 0) {
         const float x = p.v[t], y = p.v[t + 4];
         p.v[t] = reduce_f(x + y);
-        p.v[t + 4] = modmul_f(y - x, t < 8 ? z0 : z1);
+        p.v[t + 4] = modmul_lf(y - x, t < 8 ? z0 : z1);
       }
     }
   }
@@ -1031,25 +1098,36 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
     for (int t = 0; t < 8; ++t) {
       const float x = p.v[t], y = p.v[t + 8];
       p.v[t] = x + y;
-      p.v[t + 8] = modmul_f(y - x, z);
+      p.v[t + 8] = modmul_lf(y - x, z);
     }
   }
   contig_to_stride_f(p, buf, L);
 #pragma unroll
-  for (int lg = 3; lg >= 0; --lg) {
+  for (int lg = 3; lg >= (QRK_INV_FOLD ? 1 : 0); --lg) {
     const int step = 8 >> lg;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       if (((m / step) & 1) == 0) {
-        const float zeta = TABFC.z[(2 << lg) - 1 - m / (2 * step)];
+        const int zi = (2 << lg) - 1 - m / (2 * step);
         const float x = p.v[m], y = p.v[m + step];
         p.v[m] = ((lg & 1) == 1) ? reduce_f(x + y) : x + y;  // layers 4 and 6 reduce their sums
-        p.v[m + step] = modmul_f(y - x, zeta);
+        p.v[m + step] = modmul_f(y - x, TABFC.z[zi], TABFC.zq[zi]);
       }
     }
   }
+#if QRK_INV_FOLD
+  // layer 7 (step 8, zeta_1) with the scaling: |x + y|, |y - x| <= 2 * 6660, far inside the
+  // modmul_f bound for the small factors
 #pragma unroll
-  for (int m = 0; m < 16; ++m) p.v[m] = modmul_f(p.v[m], INV128F);
+  for (int m = 0; m < 8; ++m) {
+    const float x = p.v[m], y = p.v[m + 8];
+    p.v[m] = modmul_f(x + y, INV128F, (float)(INV128F / 3329.0));
+    p.v[m + 8] = modmul_f(y - x, Z1INV128F, (float)(Z1INV128F / 3329.0));
+  }
+#else
+#pragma unroll
+  for (int m = 0; m < 16; ++m) p.v[m] = modmul_f(p.v[m], INV128F, (float)(INV128F / 3329.0));
+#endif
 }
 
 // ---- base-case multiplication (FIPS 203 Alg. 11/12) on packed int16 pairs
@@ -1089,7 +1167,7 @@ __device__ __forceinline__ BOp make_bop_f(const PF16& b, int L) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const uint32_t e0 = f2bits(b.v[2 * u]), e1 = f2bits(b.v[2 * u + 1]);
-    const uint32_t g = f2bits(modmul_f(reduce_f(b.v[2 * u + 1]), TABFD.g[8 * L + u]));
+    const uint32_t g = f2bits(modmul_lf(reduce_f(b.v[2 * u + 1]), TABFD.g[8 * L + u]));
     r.b0[u] = pack16((int)e0, (int)g);
     r.b1[u] = pack16((int)e1, (int)e0);
   }
@@ -1275,9 +1353,13 @@ __device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t
 
 // ByteDecode_12 (reduced mod q) of a 384-byte NTT-domain polynomial into packed
 // pairs; `bad` collects the FIPS 203 section 7.2 modulus-check failure.
+__device__ __forceinline__ PK8 decode12_w(uint64_t a, uint64_t b, uint64_t c, bool& bad);
 __device__ __forceinline__ PK8 decode12(const uint8_t* __restrict__ src, bool& bad, int L) {
   const uint64_t* s = (const uint64_t*)(src + 24 * L);
-  const uint64_t a = s[0], b = s[1], c = s[2];
+  return decode12_w(s[0], s[1], s[2], bad);
+}
+// ByteDecode_12 of this lane's 24 bytes already in registers (a, b, c little-endian)
+__device__ __forceinline__ PK8 decode12_w(uint64_t a, uint64_t b, uint64_t c, bool& bad) {
   int v[16];
   split12((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, v);
   split12((uint32_t)(b >> 32), (uint32_t)c, (uint32_t)(c >> 32), v + 8);
@@ -1516,15 +1598,17 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
   // QRK_ENC_PREFETCH: row i+1's matrix entries and the next CBD words are loaded one row
   // ahead (latency hidden inside the wave); 0: each entry is loaded as the basemul needs it
-  // (fewer live registers, latency hidden by more resident waves).
+  // (fewer live registers, latency hidden by more resident waves).  Issuing the first row's
+  // entries before the K NTT(y_j) instead was 3 % slower (profiles/r3/ab_core_arith_c.jsonl).
 #if QRK_ENC_PREFETCH
   PK8 an[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)j * Cx + hxs, L);
 #endif
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
-#pragma unroll 1
-  for (int i = 0; i < K; ++i) {
+  // one u-row; LAST: the final row (QRK_EK_PREFETCH peels it, so its prefetch is t_hat's words)
+  auto row = [&](int i, auto last_t) {
+    constexpr bool LAST = decltype(last_t)::value;
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
@@ -1537,9 +1621,20 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
 #endif
     const CbdRaw ecur = er;
 #if QRK_ENC_PREFETCH
-    if (i + 1 < K) {
+    if (!LAST) {
+      if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * Cx + hxs, L);
+        for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * Cx + hxs, L);
+      }
+    } else {
+      // last row: the matrix registers are free, so t_hat's 24 bytes per lane and row (for v
+      // below) are loaded into them here, one row's NTT^-1 ahead of their use
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint2* e = (const uint2*)(ek + 384 * j + 24 * L);
+        const uint2 a = e[0], b = e[1], c = e[2];
+        an[j].w[0] = a.x, an[j].w[1] = a.y, an[j].w[2] = b.x, an[j].w[3] = b.y, an[j].w[4] = c.x, an[j].w[5] = c.y;
+      }
     }
 #endif
     er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
@@ -1560,7 +1655,15 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
       flush_cmp<DU>(g, cw, diff, L);
     else
       flush_bits<DU>(g, c + 32 * DU * i, nullptr, diff, active, L);
-  }
+  };
+#if QRK_ENC_PREFETCH && QRK_EK_PREFETCH
+#pragma unroll 1
+  for (int i = 0; i < K - 1; ++i) row(i, std::false_type{});
+  row(K - 1, std::true_type{});
+#else
+#pragma unroll 1
+  for (int i = 0; i < K; ++i) row(i, std::false_type{});
+#endif
   SS_MARK(TW == 16 && L == 0, 6);
   // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
   {
@@ -1570,7 +1673,13 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
+#if QRK_ENC_PREFETCH && QRK_EK_PREFETCH
+      const uint64_t a = ((uint64_t)an[j].w[1] << 32) | an[j].w[0], b = ((uint64_t)an[j].w[3] << 32) | an[j].w[2],
+                     c = ((uint64_t)an[j].w[5] << 32) | an[j].w[4];
+      basemul_acc(acc, decode12_w(a, b, c, bad), yb[j]);
+#else
       basemul_acc(acc, decode12(ek + 384 * j, bad, L), yb[j]);
+#endif
     }
     PF16 vf;
 #pragma unroll
@@ -1636,6 +1745,11 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   bool bad = false;
 #pragma unroll 1
   for (int j = 0; j < K; ++j) {
+#if QRK_DK_PREFETCH
+    // s_hat_j's 24 bytes per lane, issued before the NTT that precedes their use
+    const uint2* e = (const uint2*)(dk + 384 * j + 24 * L);
+    const uint2 da = e[0], db = e[1], dc = e[2];
+#endif
     P16 u;
     load_bits<DU>(u, c + 32 * DU * j, g, L);
     PF16 uf;
@@ -1643,7 +1757,13 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
     for (int t = 0; t < 16; ++t) uf.v[t] = i2f(decompress<DU>(u.v[t]));
     contig_to_stride_f(uf, (float*)g.poly, L);
     ntt_fwd_f<true>(uf, (float*)g.poly, L);
+#if QRK_DK_PREFETCH
+    basemul_acc(acc,
+                decode12_w(((uint64_t)da.y << 32) | da.x, ((uint64_t)db.y << 32) | db.x, ((uint64_t)dc.y << 32) | dc.x, bad),
+                make_bop_f(uf, L));
+#else
     basemul_acc(acc, decode12(dk + 384 * j, bad, L), make_bop_f(uf, L));
+#endif
   }
   PF16 w;
 #pragma unroll
