@@ -129,6 +129,7 @@ struct qrk_ctx {
   size_t hstage_bytes = 0;
   hipStream_t aux = nullptr;  // side stream for independent kernel chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_sub[8] = {};
   uint8_t* hs_scratch = nullptr;  // handshake driver: ephemeral sk / ss of one chunk
   size_t hs_scratch_bytes = 0;
   uint8_t* dio = nullptr;         // host-pointer calls: packed device inputs | outputs
@@ -359,6 +360,8 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     hipError_t e2 = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
     hipError_t e3 = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail("cannot create side stream/events");
+    for (auto& ev : ctx->ev_sub)
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail("cannot create side stream/events");
   }
   Streams S;
   S.main = st;
@@ -373,6 +376,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   S.side = (QRK_FIX_SIDE && ctx->streams != 1) ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
+  for (int i = 0; i < 8; ++i) S.sub[i] = ctx->ev_sub[i];
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
@@ -809,6 +813,8 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  for (auto ev : ctx->ev_sub)
+    if (ev) (void)hipEventDestroy(ev);
   if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
   delete ctx;
 }

@@ -37,7 +37,14 @@ namespace mlkem {
 
 constexpr int Q = 3329;
 constexpr int QINV = 62209;  // q^-1 mod 2^16
-constexpr int XOF_W = 64;    // 256 int16 sampled coefficients (512 B) per matrix entry
+// QRK_XOF_PACK12 1: the batched SampleNTT output holds 12-bit coefficients (384 B per matrix
+// entry, 8 per 12-byte chunk) instead of int16 (512 B): the encrypt core waits on memory, not on
+// the VALU (SQ wait_any 0.28-0.35 after the round-3 arithmetic cut its VALU instructions 20 % with
+// no change in time), and the matrix is 58 % of its HBM reads.
+#ifndef QRK_XOF_PACK12
+#define QRK_XOF_PACK12 1
+#endif
+constexpr int XOF_W = QRK_XOF_PACK12 ? 48 : 64;  // u64 words per matrix entry in scratch
 constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
 constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
 
@@ -229,6 +236,25 @@ __device__ __forceinline__ int compress(int x) {
   const uint32_t y = ((uint32_t)x << D) + (Q / 2);
   return (int)(__umulhi(y, 1290168u) & ((1u << D) - 1));
 }
+// Compress_d of any exact fp32 integer v congruent to x mod q, |v| <= 4091 (no reduction first):
+// fma(v, fl(2^d / q), MAGIC) rounds v 2^d / q to an integer whose low d bits are
+// round(x 2^d / q) mod 2^d (adding q to v adds 2^d).  Correct rounding: v 2^(d+1) is even and
+// (2k + 1) q odd, so v 2^d / q is at least 1 / (2q) = 1.5e-4 from every half-integer, and the
+// constant's relative error 2^-24 moves it by at most 2517 * 2^-24 < 1.5e-4 for
+// |v 2^d / q| <= 2517.  Two full-rate ops where canon_f + compress spent about twelve
+// (QRK_COMPRESS_F 0).
+#ifndef QRK_COMPRESS_F
+#define QRK_COMPRESS_F 1
+#endif
+template <int D>
+__device__ __forceinline__ int compress_f(float v) {
+#if QRK_COMPRESS_F
+  constexpr float C = (float)((double)(1 << D) / 3329.0);
+  return (int)(__float_as_uint(__builtin_fmaf(v, C, MAGIC)) & ((1u << D) - 1));
+#else
+  return compress<D>(canon_f(v));
+#endif
+}
 template <int D>
 __device__ __forceinline__ int decompress(int y) {
   return (int)(((uint32_t)Q * (uint32_t)y + (1u << (D - 1))) >> D);
@@ -326,6 +352,10 @@ __host__ __device__ __forceinline__ size_t xwrap(size_t inst) { return QRK_TIMIN
 #ifndef QRK_EK_PREFETCH
 #define QRK_EK_PREFETCH 1
 #endif
+// QRK_CT_PREFETCH 1: the decrypt core loads the ciphertext's next row one row ahead
+#ifndef QRK_CT_PREFETCH
+#define QRK_CT_PREFETCH 0
+#endif
 // QRK_DK_PREFETCH 1: the decrypt core issues s_hat_j's load before u_j's NTT
 #ifndef QRK_DK_PREFETCH
 #define QRK_DK_PREFETCH 1
@@ -358,17 +388,46 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 #ifndef QRK_XOF_PIPE
 #define QRK_XOF_PIPE 1
 #endif
+// One 8-coefficient chunk of the batched SampleNTT output: 16 bytes of int16, or 12 bytes of
+// 12-bit fields (QRK_XOF_PACK12); chunk c of entry i at ((i / TW) 32 + c) TW + i % TW units.
+struct U3 {
+  uint32_t x, y, z;
+};
+#if QRK_XOF_PACK12
+typedef U3 XUnit;
+#else
+typedef uint4 XUnit;
+#endif
+// r[j]: the chunk's coefficients (< 2^12, from the ring)
+__device__ __forceinline__ void chunk_store(XUnit* dst, const uint32_t r[8]) {
+#if QRK_XOF_PACK12
+  U3 w;
+  w.x = r[0] | (r[1] << 12) | (r[2] << 24);
+  w.y = (r[2] >> 8) | (r[3] << 4) | (r[4] << 16) | (r[5] << 28);
+  w.z = (r[5] >> 4) | (r[6] << 8) | (r[7] << 20);
+  *dst = w;
+#else
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[2 * j + 1], 16, r[2 * j]);
+  *dst = make_uint4(w[0], w[1], w[2], w[3]);
+#endif
+}
+__device__ __forceinline__ void chunk_fill(XUnit* dst, uint32_t f) {  // timing probes only
+#if QRK_XOF_PACK12
+  *dst = U3{f, f, f};
+#else
+  *dst = make_uint4(f, f, f, f);
+#endif
+}
 struct XofPend {
   uint32_t r[8];  // the chunk's ring entries, in order
   int ch = -1;    // its chunk index, -1: nothing pending
 };
 template <int TW = 64>
-__device__ __forceinline__ void xof_pend_store(XofPend& pd, uint4* dst) {
+__device__ __forceinline__ void xof_pend_store(XofPend& pd, XUnit* dst) {
   if (pd.ch >= 0) {
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = lshl_or(pd.r[2 * j + 1], 16, pd.r[2 * j]);
-    dst[pd.ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
+    chunk_store(dst + pd.ch * TW, pd.r);
     pd.ch = -1;
   }
 }
@@ -381,7 +440,7 @@ __device__ __forceinline__ void xof_pend_store(XofPend& pd, uint4* dst) {
 // v_cmp + v_cndmask pair (about three issue slots, profiles/r1/valu_peak_r1b.json) -- and
 // P >> 9 = cnt for every cnt <= 511, so bits 9-12 of P index the ring entry directly.
 template <int TW = 64>
-__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst,
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, XUnit* dst,
                                               XofPend&) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
   uint32_t P = 511u * (uint32_t)(cnt + 1);
@@ -405,17 +464,17 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     const int ch = before >> 3;
     if ((now >> 3) != ch && ch < 32) {
       const uint32_t* r = ring + (ch & 1) * 8 * 128;
-      uint32_t w[4];
+      uint32_t w[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 128], 16, r[(2 * j) * 128]);
-      dst[ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
+      for (int j = 0; j < 8; ++j) w[j] = r[j * 128];
+      chunk_store(dst + ch * TW, w);
     }
   }
   cnt = (int)(P >> 9);
 }
 #else
 template <int TW = 64>
-__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, uint4* dst,
+__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, XUnit* dst,
                                               XofPend& pd) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
 #if QRK_XOF_TIMING_ONLY >= 2
@@ -471,15 +530,15 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     if ((cnt >> 3) != ch && ch < 32) {
 #endif
       const uint32_t* r = ring + (ch & 1) * 8 * 64;
-      uint32_t w[4];
+      uint32_t w[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[(2 * j + 1) * 64], 16, r[(2 * j) * 64]);
-      dst[ch * TW] = make_uint4(w[0], w[1], w[2], w[3]);
+      for (int j = 0; j < 8; ++j) w[j] = r[j * 64];
+      chunk_store(dst + ch * TW, w);
     }
 #endif
   }
 #if QRK_XOF_TIMING_ONLY >= 2
-  if (tsink == 0x12345678u) dst[0] = make_uint4(tsink, tsink, tsink, tsink);
+  if (tsink == 0x12345678u) chunk_fill(dst, tsink);
 #endif
 }
 
@@ -522,7 +581,7 @@ __device__ __forceinline__ void xof_init(KState& s, const uint64_t* __restrict__
 
 // squeeze + compact blocks: exactly NB of them (ALL = false), or until 256 values (ALL = true)
 template <bool ALL, int NB, int TW = 64>
-__device__ __forceinline__ void xof_blocks(KState& s, int& cnt, uint4* __restrict__ dst, char* ring_all, uint32_t rb) {
+__device__ __forceinline__ void xof_blocks(KState& s, int& cnt, XUnit* __restrict__ dst, char* ring_all, uint32_t rb) {
   XofPend pd;
 #pragma unroll 1
   for (int b = 0; b < NB && (!ALL || cnt < 256); ++b) {
@@ -543,7 +602,7 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, uint4* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) cnt += c[e] < Q ? 1 : 0;
     }
-    dst[b * TW] = make_uint4(cnt, cnt, cnt, cnt);
+    chunk_fill(dst + b * TW, (uint32_t)cnt);
     if (b == NB - 1) cnt = 256;
 #elif QRK_XOF_TIMING_ONLY == 1
     // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
@@ -551,7 +610,7 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, uint4* __restric
     uint32_t f = 0;
 #pragma unroll
     for (int w = 0; w < 21; ++w) f ^= s.a[w].lo ^ s.a[w].hi;
-    dst[b * TW] = make_uint4(f, f, f, f);
+    chunk_fill(dst + b * TW, f);
     cnt = 256;
 #else
     compact_block<TW>(s, ring_all, rb, cnt, dst, pd);
@@ -569,9 +628,9 @@ __device__ __forceinline__ uint32_t* ring_entry(char* ring_all, uint32_t rb, int
 // exactly 3 blocks (returns the count, < 256 when a 4th block is needed); ALL = true: as many
 // blocks as it takes.  rb = this lane's ring column (see compact_block).
 template <int K, bool ALL, int TW = 64>
-__device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, uint4* __restrict__ out,
+__device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, XUnit* __restrict__ out,
                                          char* ring_all, uint32_t rb) {
-  uint4* dst = out + (inst / TW) * 32 * TW + (inst % TW);
+  XUnit* dst = out + (inst / TW) * 32 * TW + (inst % TW);
   KState s;
   xof_init(s, rho, xy, K);
   int cnt = 0;
@@ -585,7 +644,7 @@ __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int x
 // from-scratch path), so the rare 4th block never idles a whole wave.
 template <int K, bool FIX>
 __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
-                                             size_t n, size_t C, uint4* __restrict__ out,
+                                             size_t n, size_t C, XUnit* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix,
                                              uint32_t* __restrict__ fixrec) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
@@ -637,7 +696,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (base + j < cnt) *ring_entry(ring, rb, base + j) = rec[52 + j];
-        uint4* dst = out + (inst / XTW) * 32 * XTW + (inst % XTW);
+        XUnit* dst = out + (inst / XTW) * 32 * XTW + (inst % XTW);
         xof_blocks<true, MAX_XOF_BLOCKS, XTW>(s, cnt, dst, ring, rb);
       } else {
         const size_t inst = fix[r - cap];
@@ -844,11 +903,25 @@ constexpr int PBUF = 272;
 // group stride is 368 dwords = 16 (mod 32): the two 16-lane groups that share a ds_* bank
 // half (lanes 0-31 / 32-63) then use disjoint bank sets for every access pattern above.
 constexpr int RAWW = 44;
-constexpr int GPAD = 8;
+// QRK_RAW_ALIAS 1: the byte staging shares the polynomial image's words.  No code path holds a
+// polynomial in the image while it stages bytes: pack_bits / flush_* run after the last
+// transpose of a row and end with a group sync before the next transpose, load_bits ends with one
+// before its caller's first transpose.  1088 B per group instead of 1472 (the encrypt core's
+// SampleNTT prefetch buffer needs the room at 4 waves / SIMD).
+#ifndef QRK_RAW_ALIAS
+#define QRK_RAW_ALIAS 0
+#endif
 struct GroupLds {
+#if QRK_RAW_ALIAS
+  union {
+    int poly[PBUF];
+    uint64_t raw[RAWW];
+  };
+#else
   int poly[PBUF];
   uint64_t raw[RAWW];
-  int pad[GPAD];
+  int pad[8];
+#endif
 };
 static_assert(sizeof(GroupLds) / 4 % 32 == 16, "group stride must be 16 mod 32 dwords");
 constexpr int GROUPS = 16;  // 256 threads
@@ -1235,17 +1308,33 @@ __device__ __forceinline__ void cbd_f(PF16& p, const CbdRaw& r) {
   }
 }
 
-// Group-cooperative load of 16*D*2 bytes at src (4-byte aligned) into the raw
-// stage, then lane L unpacks its 16 D-bit fields (bits 16*D*L ...).
+// A group's 16*D*2 bytes at src (4-byte aligned) as this lane's share of dwords (L, L + 16, ...),
+// loaded ahead of load_bits_r; DL <= D reads a shorter (DL-bit) encoding into the same shape.
 template <int D>
-__device__ __forceinline__ void load_bits(P16& p, const uint8_t* __restrict__ src, GroupLds& g, int L) {
+struct RawW {
+  uint32_t w[(8 * D + 15) / 16];
+};
+template <int D, int DL = D>
+__device__ __forceinline__ RawW<D> raw_load(const uint8_t* __restrict__ src, int L) {
+  RawW<D> r;
+  const uint32_t* s32 = (const uint32_t*)src;
+#pragma unroll
+  for (int i = 0; i < (8 * D + 15) / 16; ++i) {
+    const int idx = L + 16 * i;
+    r.w[i] = idx < 8 * DL ? s32[idx] : 0u;
+  }
+  return r;
+}
+// Group-cooperative stage of 16*D*2 bytes (already loaded, raw_load) into the raw stage, then lane
+// L unpacks its 16 D-bit fields (bits 16*D*L ...).
+template <int D, int DX>
+__device__ __forceinline__ void load_bits_r(P16& p, const RawW<DX>& r, GroupLds& g, int L) {
   constexpr int NDW = 8 * D;  // dwords for 256 D-bit values
   uint32_t* st = (uint32_t*)g.raw;
-  const uint32_t* s32 = (const uint32_t*)src;
 #pragma unroll
   for (int i = 0; i < (NDW + 15) / 16; ++i) {
     const int idx = L + 16 * i;
-    if (idx < NDW) st[idx] = s32[idx];
+    if (idx < NDW) st[idx] = r.w[i];
   }
   gsync();
   // this lane's 2D bytes start at byte 2*D*L
@@ -1270,6 +1359,10 @@ __device__ __forceinline__ void load_bits(P16& p, const uint8_t* __restrict__ sr
     p.v[t] = (int)(v & ((1u << D) - 1));
   }
   gsync();
+}
+template <int D>
+__device__ __forceinline__ void load_bits(P16& p, const uint8_t* __restrict__ src, GroupLds& g, int L) {
+  load_bits_r<D>(p, raw_load<D>(src, L), g, L);
 }
 
 // Pack lane L's 16 D-bit fields into the raw stage at byte 2*D*L (whole group: 32*D bytes).
@@ -1343,12 +1436,58 @@ __device__ __forceinline__ void flush_cmp(GroupLds& g, const CmpWords<D>& c, uin
 
 // SampleNTT consumer: lane L loads coefficients 16L..16L+15 (chunks 2L, 2L+1)
 // of the producer's compacted output -- contiguous layout, no parsing.
-template <int TW = 64>
-__device__ __forceinline__ PK8 load_sampled(const uint4* __restrict__ xs, size_t inst, int L) {
+// The batched producer's 12-bit chunks (QRK_XOF_PACK12), spread back to int16 pairs: a pair is 24
+// consecutive bits x, (x & 0xFFF) | (x << 4 & 0x0FFF0000) -- about 3 VALU per pair.
+__device__ __forceinline__ PK8 unpack12(const U3& u, const U3& v) {
+  const uint32_t w[6] = {u.x, u.y, u.z, v.x, v.y, v.z};
+  PK8 r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t a = w[3 * h], b = w[3 * h + 1], c = w[3 * h + 2];
+    const uint32_t x[4] = {a, __builtin_amdgcn_alignbit(b, a, 24), __builtin_amdgcn_alignbit(c, b, 16), c >> 8};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r.w[4 * h + k] = (x[k] & 0xFFFu) | ((x[k] << 4) & 0x0FFF0000u);
+  }
+  return r;
+}
+template <int TW = 64, bool P12 = false>
+__device__ __forceinline__ PK8 load_sampled(const void* __restrict__ xs_, size_t inst, int L) {
   if (TW == XTW) inst = xwrap(inst);
-  const uint4* base = xs + (inst / TW) * 32 * TW + (inst % TW);
-  const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
-  return PK8{{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}};
+  if constexpr (P12) {
+    const U3* base = (const U3*)xs_ + (inst / TW) * 32 * TW + (inst % TW);
+    return unpack12(base[(2 * L) * TW], base[(2 * L + 1) * TW]);
+  } else {
+    const uint4* base = (const uint4*)xs_ + (inst / TW) * 32 * TW + (inst % TW);
+    const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
+    return PK8{{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w}};
+  }
+}
+// the batched cores' view of the SampleNTT output
+#define LOAD_XOF(TW_, inst) load_sampled<(TW_) == 64 ? XTW : (TW_), (TW_) == 64 && QRK_XOF_PACK12>(xof, (inst), L)
+
+// QRK_ENC_GLDS 1 (needs QRK_XOF_PACK12): the batched encrypt core prefetches the next row's matrix
+// entries (and, for v, t_hat's words) global -> LDS with global_load_lds_dwordx3 into a per-wave
+// buffer (lane l's 12 bytes at base + 12 l, read back by the same lane) instead of into 24 VGPRs,
+// so the core fits 4 waves / SIMD.  The compiler does not order LDS reads after an LDS-DMA, hence
+// the explicit vmcnt(0) before the buffer is read.
+#ifndef QRK_ENC_GLDS
+#define QRK_ENC_GLDS 0
+#endif
+__device__ __forceinline__ void glds12(const void* gsrc, U3* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 12, 0, 0);
+}
+__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// issue row `row`'s K entries (inst = (row K + j) Cx + hxs) into the wave's buffer
+template <int K>
+__device__ __forceinline__ void glds_row(const void* xof, size_t Cx, size_t hxs, int row, int L, U3* ab) {
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const size_t inst = xwrap(((size_t)row * K + j) * Cx + hxs);
+    const U3* base = (const U3*)xof + (inst / XTW) * 32 * XTW + (inst % XTW);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) glds12(base + (2 * L + c) * XTW, ab + (2 * j + c) * 64);
+  }
 }
 
 // ByteDecode_12 (reduced mod q) of a 384-byte NTT-domain polynomial into packed
@@ -1414,11 +1553,12 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
+  size_t fix_cap;        // list capacity K^2 C; 8 spare words follow it (QRK_SPLIT part counters)
   uint32_t* fixrec;      // SampleNTT resume records (QRK_XOF_RESUME)
   uint64_t* rho;         // QRK_RHO_COMPACT: every handshake's rho, 32 B apart
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 2 +
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 4 +
          xof_rec_cap(K, C) * XOF_REC_WORDS / 2 + 4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
@@ -1438,7 +1578,8 @@ inline ScratchView carve(void* base, int K, size_t C) {
   p += 4 * C;
   v.nfix = (uint32_t*)p;
   v.fix = v.nfix + 2;
-  p += ((size_t)K * K * C + 2) / 2 + 2;
+  v.fix_cap = (size_t)K * K * C;
+  p += ((size_t)K * K * C + 2) / 2 + 4;
   v.fixrec = (uint32_t*)p;
   p += xof_rec_cap(K, C) * XOF_REC_WORDS / 2;
   v.rho = p;
@@ -1520,7 +1661,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K) * Cx + hxs, L);
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K) * Cx + hxs);
   CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
@@ -1532,7 +1673,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(j * K + i + 1) * Cx + hxs, L);
+      for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K + i + 1) * Cx + hxs);
       er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
     }
     PF16 ef;
@@ -1568,8 +1709,13 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
                                                       uint8_t* __restrict__ ct, int32_t* __restrict__ status,
                                                       const uint64_t* __restrict__ kprime,
-                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g) {
+                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g,
+                                                      U3* ab = nullptr) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
+  // ab: this wave's LDS prefetch buffer (QRK_ENC_GLDS; the batched kernel only)
+  constexpr bool GL = QRK_ENC_GLDS && QRK_XOF_PACK12 && QRK_ENC_PREFETCH && QRK_EK_PREFETCH && TW == 64;
+  const int wl = threadIdx.x & 63;
+  (void)wl, (void)ab;
   const bool active = hs_raw < n;
   const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see QRK_XOF_SUB)
   const size_t hs = off + hl;                 // index in the chunk
@@ -1579,6 +1725,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
+  if constexpr (GL) glds_row<K>(xof, Cx, hxs, 0, L, ab);  // row 0's entries land during the NTT(y_j)
 
   BOp yb[K];
   {
@@ -1602,8 +1749,10 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   // entries before the K NTT(y_j) instead was 3 % slower (profiles/r3/ab_core_arith_c.jsonl).
 #if QRK_ENC_PREFETCH
   PK8 an[K];
+  if constexpr (!GL) {
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)j * Cx + hxs, L);
+    for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * Cx + hxs);
+  }
 #endif
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
   // one u-row; LAST: the final row (QRK_EK_PREFETCH peels it, so its prefetch is t_hat's words)
@@ -1612,19 +1761,37 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
+    if constexpr (GL) {
+      glds_wait();
+#pragma unroll
+      for (int j = 0; j < K; ++j) basemul_acc(acc, unpack12(ab[(2 * j) * 64 + wl], ab[(2 * j + 1) * 64 + wl]), yb[j]);
+    } else {
 #if QRK_ENC_PREFETCH
 #pragma unroll
-    for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
+      for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
 #else
 #pragma unroll
-    for (int j = 0; j < K; ++j) basemul_acc(acc, load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)(i * K + j) * Cx + hxs, L), yb[j]);
+      for (int j = 0; j < K; ++j) basemul_acc(acc, LOAD_XOF(TW, (size_t)(i * K + j) * Cx + hxs), yb[j]);
 #endif
+    }
     const CbdRaw ecur = er;
+    if constexpr (GL) {
+      // the buffer's reads have landed in registers (the basemuls used them): refill it
+      if (!LAST && i + 1 < K) {
+        glds_row<K>(xof, Cx, hxs, i + 1, L, ab);
+      } else if (LAST) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          glds12(ek + 384 * j + 24 * L, ab + (2 * j) * 64);
+          glds12(ek + 384 * j + 24 * L + 12, ab + (2 * j + 1) * 64);
+        }
+      }
+    } else {
 #if QRK_ENC_PREFETCH
     if (!LAST) {
       if (i + 1 < K) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) an[j] = load_sampled<TW == 64 ? XTW : TW>((const uint4*)xof, (size_t)((i + 1) * K + j) * Cx + hxs, L);
+        for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)((i + 1) * K + j) * Cx + hxs);
       }
     } else {
       // last row: the matrix registers are free, so t_hat's 24 bytes per lane and row (for v
@@ -1637,6 +1804,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
       }
     }
 #endif
+    }
     er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
     PF16 uf;
 #pragma unroll
@@ -1649,7 +1817,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     cbd_f<P<K>::ETA2>(ef, ecur);
     P16 u;
 #pragma unroll
-    for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon_f(uf.v[t] + ef.v[t]));
+    for (int t = 0; t < 16; ++t) u.v[t] = compress_f<DU>(uf.v[t] + ef.v[t]);
     pack_bits<DU>(u, g, L);
     if (MODE)
       flush_cmp<DU>(g, cw, diff, L);
@@ -1674,8 +1842,17 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
 #pragma unroll
     for (int j = 0; j < K; ++j) {
 #if QRK_ENC_PREFETCH && QRK_EK_PREFETCH
-      const uint64_t a = ((uint64_t)an[j].w[1] << 32) | an[j].w[0], b = ((uint64_t)an[j].w[3] << 32) | an[j].w[2],
-                     c = ((uint64_t)an[j].w[5] << 32) | an[j].w[4];
+      uint32_t w[6];
+      if constexpr (GL) {
+        if (j == 0) glds_wait();
+        const U3 u = ab[(2 * j) * 64 + wl], v = ab[(2 * j + 1) * 64 + wl];
+        w[0] = u.x, w[1] = u.y, w[2] = u.z, w[3] = v.x, w[4] = v.y, w[5] = v.z;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) w[t] = an[j].w[t];
+      }
+      const uint64_t a = ((uint64_t)w[1] << 32) | w[0], b = ((uint64_t)w[3] << 32) | w[2],
+                     c = ((uint64_t)w[5] << 32) | w[4];
       basemul_acc(acc, decode12_w(a, b, c, bad), yb[j]);
 #else
       basemul_acc(acc, decode12(ek + 384 * j, bad, L), yb[j]);
@@ -1694,7 +1871,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const float mu = ((mb >> t) & 1) ? (float)((Q + 1) / 2) : 0.0f;
-      v.v[t] = compress<DV>(canon_f(vf.v[t] + ef.v[t] + mu));
+      v.v[t] = compress_f<DV>(vf.v[t] + ef.v[t] + mu);
     }
     pack_bits<DV>(v, g, L);
     flush_bits<DV>(g, c + 32 * DU * K, MODE ? c + 32 * DU * K : nullptr, diff, active, L);
@@ -1716,7 +1893,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   SS_MARK(TW == 16 && L == 0, 7);
 }
 template <int K, int MODE>
-__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? QRK_WPE_CORE : (QRK_ENC_GLDS ? 4 : 3)))) void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
                                                       const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
@@ -1726,8 +1903,14 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_encrypt_core(size_t n, si
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
+#if QRK_ENC_GLDS
+  __shared__ U3 abuf[4 * 2 * K * 64];
+  U3* ab = abuf + (threadIdx.x >> 6) * 2 * K * 64;
+#else
+  U3* ab = nullptr;
+#endif
   encrypt_core_hs<K, MODE>(n, C, Cx, off, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
-                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi], ab);
 }
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
@@ -1743,6 +1926,10 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = 0;
   bool bad = false;
+#if QRK_CT_PREFETCH
+  // the ciphertext rows are loaded one row ahead (u_0 here, then u_{j+1} or v during row j)
+  RawW<DU> cur = raw_load<DU>(c, L);
+#endif
 #pragma unroll 1
   for (int j = 0; j < K; ++j) {
 #if QRK_DK_PREFETCH
@@ -1751,7 +1938,17 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
     const uint2 da = e[0], db = e[1], dc = e[2];
 #endif
     P16 u;
+#if QRK_CT_PREFETCH
+    RawW<DU> nxt;
+    if (j + 1 < K)
+      nxt = raw_load<DU>(c + 32 * DU * (j + 1), L);
+    else
+      nxt = raw_load<DU, DV>(c + 32 * DU * K, L);
+    load_bits_r<DU>(u, cur, g, L);
+    cur = nxt;
+#else
     load_bits<DU>(u, c + 32 * DU * j, g, L);
+#endif
     PF16 uf;
 #pragma unroll
     for (int t = 0; t < 16; ++t) uf.v[t] = i2f(decompress<DU>(u.v[t]));
@@ -1771,12 +1968,15 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   ntt_inv_f(w, (float*)g.poly, L);
   stride_to_contig_f(w, (float*)g.poly, L);
   P16 v;
+#if QRK_CT_PREFETCH
+  load_bits_r<DV>(v, cur, g, L);
+#else
   load_bits<DV>(v, c + 32 * DU * K, g, L);
+#endif
   uint32_t bits = 0;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
-    const int x = canon_f(i2f(decompress<DV>(v.v[t])) - w.v[t]);
-    bits |= (uint32_t)compress<1>(x) << t;
+    bits |= (uint32_t)compress_f<1>(i2f(decompress<DV>(v.v[t])) - w.v[t]) << t;
   }
   if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
 }
@@ -1993,7 +2193,7 @@ __device__ __forceinline__ void enc_row_one(const OneLds& sl, int i, uint8_t* __
   cbd_f<P<K>::ETA2>(ef, er);
   P16 u;
 #pragma unroll
-  for (int t = 0; t < 16; ++t) u.v[t] = compress<DU>(canon_f(uf.v[t] + ef.v[t]));
+  for (int t = 0; t < 16; ++t) u.v[t] = compress_f<DU>(uf.v[t] + ef.v[t]);
   pack_bits<DU>(u, g, L);
   if (MODE)
     flush_cmp<DU>(g, cw, diff, L);
@@ -2026,7 +2226,7 @@ __device__ __forceinline__ bool enc_v_one(const OneLds& sl, const uint8_t* __res
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
     const float mu = ((mb >> t) & 1) ? (float)((Q + 1) / 2) : 0.0f;
-    v.v[t] = compress<DV>(canon_f(vf.v[t] + ef.v[t] + mu));
+    v.v[t] = compress_f<DV>(vf.v[t] + ef.v[t] + mu);
   }
   pack_bits<DV>(v, g, L);
   flush_bits<DV>(g, c + 32 * DU * K, MODE ? c + 32 * DU * K : nullptr, diff, true, L);
@@ -2434,10 +2634,15 @@ inline void join(const Streams& s) {
 // the core reads the sampled matrix
 template <int K>
 void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st,
-                const Streams* fixside = nullptr) {
-  (void)hipMemsetAsync(v.nfix, 0, 4, st);
+                const Streams* fixside = nullptr, int part = -1) {
+  // part >= 0 (QRK_SPLIT): SampleNTT part `part` of a split chunk, C = the part's stride, with its own
+  // matrix region, fix-up list and counter (the counters sit in the 8 spare words after the list)
+  XUnit* out = (XUnit*)(part < 0 ? v.xof : v.xof + (size_t)part * K * K * C * XOF_W);
+  uint32_t* fix = part < 0 ? v.fix : v.fix + (size_t)part * K * K * C;
+  uint32_t* nfix = part < 0 ? v.nfix : v.fix + v.fix_cap + part;
+  (void)hipMemsetAsync(nfix, 0, 4, st);
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
-             C, (uint4*)v.xof, v.fix, v.nfix, v.fixrec);
+             C, out, fix, nfix, v.fixrec);
   hipStream_t fs = st;
   if (fixside) {
     (void)hipEventRecord(fixside->fork, st);
@@ -2448,8 +2653,8 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   // the fix-up is latency-bound (4+ sequential permutations per lane), a second grid-stride
   // pass would double it
   const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
-  QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C,
-             (uint4*)v.xof, v.fix, v.nfix, v.fixrec);
+  QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C, out,
+             fix, nfix, v.fixrec);
   if (fixside) (void)hipEventRecord(fixside->join, fs);
 }
 inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }
@@ -2527,6 +2732,64 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   return hipGetLastError();
 }
 
+// QRK_SPLIT P > 1: at full chunks (single-stream schedule with a side stream) the SampleNTT pass
+// runs as P parts on the side stream while the main stream runs the front hash, the PRFs and then
+// the encrypt core part by part, each part's core waiting only for its own matrix.  k_xof is
+// VALU-bound and the encrypt core waits on memory 28-35 % of its time (SQ), so a core part
+// overlaps the next SampleNTT part instead of running alone.
+#ifndef QRK_SPLIT
+#define QRK_SPLIT 4
+#endif
+static_assert(QRK_SPLIT >= 0 && QRK_SPLIT <= 8, "QRK_SPLIT parts: one event and one spare fix-up counter each, 8 at most");
+#ifndef QRK_SPLIT_MIN
+#define QRK_SPLIT_MIN 262144
+#endif
+template <int K>
+bool split_ok(size_t n, size_t C, const Streams& s) {
+  return QRK_SPLIT > 1 && !s.aux && s.side && s.sub[QRK_SPLIT - 1] && n >= (size_t)QRK_SPLIT_MIN &&
+         C % (64 * QRK_SPLIT) == 0;
+}
+// QRK_SPLIT_LAG 1: part 0 runs on the main stream after the PRFs and the side stream's parts
+// 1..P-1 start only then, so they overlap the encrypt cores rather than the (VALU-bound) front
+// hash and PRFs; 0: the side stream starts all parts at once.
+#ifndef QRK_SPLIT_LAG
+#define QRK_SPLIT_LAG 0
+#endif
+// the SampleNTT parts; the caller's core for part q waits on s.sub[q].  Called where part 0 may
+// start: with QRK_SPLIT_LAG after the PRFs on main, else right after the rho copy.
+template <int K>
+void launch_xof_split(const RhoSrc& rs, size_t n, size_t C, const ScratchView& v, const Streams& s) {
+  const size_t Cq = C / QRK_SPLIT;
+  int q0 = 0;
+  if (QRK_SPLIT_LAG) {
+    launch_xof<K>(rs.at(0), rs.stride, std::min(Cq, n), Cq, v, s.main, nullptr, 0);
+    (void)hipEventRecord(s.sub[0], s.main);
+    q0 = 1;
+  }
+  (void)hipEventRecord(s.fork, s.main);  // after the rho copy / part 0 / the previous chunk's cores
+  (void)hipStreamWaitEvent(s.side, s.fork, 0);
+  for (int q = q0; q < QRK_SPLIT; ++q) {
+    const size_t off = (size_t)q * Cq, m = off < n ? std::min(Cq, n - off) : 0;
+    if (m) launch_xof<K>(rs.at(off), rs.stride, m, Cq, v, s.side, nullptr, q);
+    (void)hipEventRecord(s.sub[q], s.side);
+  }
+}
+template <int K, int MODE>
+void launch_core_split(size_t n, size_t C, const ScratchView& v, const Streams& s, const uint8_t* ek, size_t ek_stride,
+                       const uint8_t* m_base, size_t m_stride, uint8_t* ct, int32_t* status, const uint64_t* kprime,
+                       const uint64_t* kbar, uint8_t* ss) {
+  const size_t Cq = C / QRK_SPLIT;
+  for (int q = 0; q < QRK_SPLIT; ++q) {
+    (void)hipStreamWaitEvent(s.main, s.sub[q], 0);
+    const size_t off = (size_t)q * Cq;
+    if (off >= n) continue;
+    const size_t m = std::min(Cq, n - off);
+    QRK_LAUNCH("k_encrypt_core", s.main, (k_encrypt_core<K, MODE>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
+               dim3(256), 0, s.main, m, C, Cq, off, v.xof + (size_t)q * K * K * Cq * XOF_W, v.prf, ek, ek_stride,
+               m_base, m_stride, ct, status, kprime, kbar, ss);
+  }
+}
+
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2539,6 +2802,18 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const Streams* fs = fix_side(s);
+  if (split_ok<K>(n, C, s)) {
+    const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, true);
+    if (!QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
+    QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
+               v.seeds);
+    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+               v.seeds, n, C, 2 * K + 1, K, v.prf);
+    if (QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
+    launch_core_split<K, 0>(n, C, v, s, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
+                            nullptr);
+    return hipGetLastError();
+  }
   if (xof_sub(n)) {
     const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, true);
     QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
@@ -2589,6 +2864,19 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
     (void)hipEventRecord(fs->fork, st);
     (void)hipStreamWaitEvent(fs->side, fs->fork, 0);
     QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
+  }
+  if (split_ok<K>(n, C, s) && !jside) {
+    const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, st, true);
+    if (!QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
+    QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
+    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
+               v.seeds, v.kprime, v.kbar);
+    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
+               v.seeds, n, C, 2 * K + 1, K, v.prf);
+    if (QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
+    launch_core_split<K, 1>(n, C, v, s, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
+                            const_cast<uint8_t*>(ct), (int32_t*)nullptr, v.kprime, v.kbar, ss);
+    return hipGetLastError();
   }
   if (xof_sub(n) && !jside) {
     const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, st, true);

@@ -68,6 +68,8 @@ struct Streams {
   hipStream_t main = nullptr;
   hipStream_t aux = nullptr;  // nullptr: single-stream schedule
   hipEvent_t fork = nullptr, join = nullptr;
+  // ML-KEM split pipeline (QRK_SPLIT): one event per SampleNTT quarter on the side stream
+  hipEvent_t sub[8] = {};
   // the context's side stream even on the single-stream schedule: ML-KEM runs its SampleNTT
   // fix-up kernel there, beside the front hash (nullptr: fix-up on main)
   hipStream_t side = nullptr;
