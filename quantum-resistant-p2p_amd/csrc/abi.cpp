@@ -129,7 +129,6 @@ struct qrk_ctx {
   size_t hstage_bytes = 0;
   hipStream_t aux = nullptr;  // side stream for independent kernel chains
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_sub[8] = {};
   uint8_t* hs_scratch = nullptr;  // handshake driver: ephemeral sk / ss of one chunk
   size_t hs_scratch_bytes = 0;
   uint8_t* dio = nullptr;         // host-pointer calls: packed device inputs | outputs
@@ -295,6 +294,30 @@ static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
   return cap;
 }
 
+// Per-chunk events of the ML-KEM split pipeline (Streams::sfork / sub): created before the chunk's
+// launches and released when the scope ends -- hipEventDestroy on an event whose work is still
+// pending releases it once the work completes -- so no event is re-recorded while an earlier
+// hipStreamWaitEvent on it may still be pending on the device.
+struct SplitEvents {
+  Streams& s;
+  bool on, ok = true;
+  SplitEvents(bool enable, Streams& st) : s(st), on(enable) {
+    if (!on) return;
+    ok = hipEventCreateWithFlags(&s.sfork, hipEventDisableTiming) == hipSuccess;
+    for (auto& ev : s.sub) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+  }
+  ~SplitEvents() {
+    if (!on) return;
+    if (s.sfork) (void)hipEventDestroy(s.sfork);
+    for (auto& ev : s.sub) {
+      if (ev) (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+    s.sfork = nullptr;
+  }
+};
+
+
 // Routes QRK_LAUNCH timing to the context's timer for the scope's lifetime (nests).
 struct TimerScope {
   KernelTimer* prev;
@@ -360,8 +383,6 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     hipError_t e2 = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
     hipError_t e3 = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail("cannot create side stream/events");
-    for (auto& ev : ctx->ev_sub)
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail("cannot create side stream/events");
   }
   Streams S;
   S.main = st;
@@ -376,7 +397,6 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   S.side = (QRK_FIX_SIDE && ctx->streams != 1) ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
-  for (int i = 0; i < 8; ++i) S.sub[i] = ctx->ev_sub[i];
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
@@ -393,6 +413,9 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     hipError_t e = hipSuccess;
+    // fresh split-pipeline events for this chunk (ML-KEM Encaps / Decaps on the auto schedule)
+    SplitEvents split_ev(a.family == Family::MLKEM && op != Op::KEYPAIR && S.side && !S.aux && mlkem_split_parts(), S);
+    if (!split_ev.ok) return fail("cannot create split-pipeline events");
     if (a.family == Family::MLKEM) {
       switch (op) {
         case Op::KEYPAIR:
@@ -813,8 +836,6 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
-  for (auto ev : ctx->ev_sub)
-    if (ev) (void)hipEventDestroy(ev);
   if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
   delete ctx;
 }

@@ -57,6 +57,8 @@ size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 // ML-KEM batches up to this size run as one launch per operation with no scratch key material
 size_t mlkem_small_max();
+// ML-KEM split SampleNTT / core pipeline parts built in (QRK_SPLIT; 0 = off)
+int mlkem_split_parts();
 // ML-KEM KeyGen batches up to this size run one workgroup per SampleNTT / PRF item (latency)
 size_t mlkem_kg_multi_max();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
@@ -68,7 +70,10 @@ struct Streams {
   hipStream_t main = nullptr;
   hipStream_t aux = nullptr;  // nullptr: single-stream schedule
   hipEvent_t fork = nullptr, join = nullptr;
-  // ML-KEM split pipeline (QRK_SPLIT): one event per SampleNTT quarter on the side stream
+  // ML-KEM split pipeline (QRK_SPLIT): the fork from main and one event per SampleNTT part on the
+  // side stream -- created for each chunk and released after its launches, so no event is ever
+  // re-recorded while an earlier wait on it may still be pending
+  hipEvent_t sfork = nullptr;
   hipEvent_t sub[8] = {};
   // the context's side stream even on the single-stream schedule: ML-KEM runs its SampleNTT
   // fix-up kernel there, beside the front hash (nullptr: fix-up on main)
