@@ -72,6 +72,7 @@ static int hip_fail(const char* what, hipError_t e) {
 // ------------------------------------------------------------------ kernel timing
 namespace qrk {
 thread_local KernelTimer* g_timer = nullptr;
+thread_local hipError_t g_launch_err = hipSuccess;
 }
 
 // Pairs of HIP events recorded on the launch stream around every kernel; read
@@ -159,8 +160,10 @@ static int ctx_order(qrk_ctx* ctx, hipStream_t st) {
     if (e != hipSuccess) return hip_fail("hipEventCreate(last use)", e);
   }
   if (ctx->last_valid && ctx->last_stream != st) {  // same stream: already in order
-    hipError_t e = hipStreamWaitEvent(st, ctx->ev_last, 0);
-    if (e != hipSuccess) return hip_fail("hipStreamWaitEvent(last use)", e);
+    // host-side wait, as for the launchers' forks (fork_wait in qrkem_internal.h): the previous
+    // stream may be the caller's legacy NULL stream
+    hipError_t e = hipEventSynchronize(ctx->ev_last);
+    if (e != hipSuccess) return hip_fail("hipEventSynchronize(last use)", e);
   }
   return 0;
 }
@@ -413,6 +416,8 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     hipError_t e = hipSuccess;
+    g_launch_err = hipSuccess;
+    (void)hipGetLastError();  // clear a stale error state (e.g. a caller's hipErrorNotReady query)
     // fresh split-pipeline events for this chunk (ML-KEM Encaps / Decaps on the auto schedule)
     SplitEvents split_ev(a.family == Family::MLKEM && op != Op::KEYPAIR && S.side && !S.aux && mlkem_split_parts(), S);
     if (!split_ev.ok) return fail("cannot create split-pipeline events");
@@ -467,6 +472,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
           break;
       }
     }
+    if (e == hipSuccess) e = g_launch_err;
     if (e != hipSuccess) return hip_fail("kernel launch", e);
     // key material of this chunk (seeds, m', K', Kbar, ...) does not outlive the call
     e = cleanse_records(a, m, ctx->scratch, st);

@@ -2614,13 +2614,12 @@ inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 // after the previous chunk's core, so reused scratch is never overwritten early.
 inline void fork(const Streams& s) {
   if (!s.aux) return;
-  (void)hipEventRecord(s.fork, s.main);
-  (void)hipStreamWaitEvent(s.aux, s.fork, 0);
+  fork_wait(s.main, s.aux, s.fork);
 }
 inline void join(const Streams& s) {
   if (!s.aux) return;
-  (void)hipEventRecord(s.join, s.aux);
-  (void)hipStreamWaitEvent(s.main, s.join, 0);
+  qrk_chk(hipEventRecord(s.join, s.aux));
+  qrk_chk(hipStreamWaitEvent(s.main, s.join, 0));
 }
 
 // QRK_J_SIDE 1: Decaps' J(z || c) on the side stream beside k_xof / the decrypt core (see k_j_decaps).
@@ -2641,13 +2640,12 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   XUnit* out = (XUnit*)(part < 0 ? v.xof : v.xof + (size_t)part * K * K * C * XOF_W);
   uint32_t* fix = part < 0 ? v.fix : v.fix + (size_t)part * K * K * C;
   uint32_t* nfix = part < 0 ? v.nfix : v.fix + v.fix_cap + part;
-  (void)hipMemsetAsync(nfix, 0, 4, st);
+  qrk_chk(hipMemsetAsync(nfix, 0, 4, st));
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
              C, out, fix, nfix, v.fixrec);
   hipStream_t fs = st;
   if (fixside) {
-    (void)hipEventRecord(fixside->fork, st);
-    (void)hipStreamWaitEvent(fixside->side, fixside->fork, 0);
+    fork_wait(st, fixside->side, fixside->fork);
     fs = fixside->side;
   }
   // one lane per listed entry in a single pass for fix-up rates up to 1/64 (~0.7 % expected):
@@ -2656,11 +2654,11 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
   QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C, out,
              fix, nfix, v.fixrec);
-  if (fixside) (void)hipEventRecord(fixside->join, fs);
+  if (fixside) qrk_chk(hipEventRecord(fixside->join, fs));
 }
 inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }
 inline void fix_join(const Streams* fs) {
-  if (fs) (void)hipStreamWaitEvent(fs->main, fs->join, 0);
+  if (fs) qrk_chk(hipStreamWaitEvent(fs->main, fs->join, 0));
 }
 
 // QRK_XOF_SUB S > 0: SampleNTT and the core that consumes it run in sub-chunks of S handshakes
@@ -2761,7 +2759,7 @@ inline bool debug_poison() {
 }
 template <int K>
 void poison_xof(size_t C, const ScratchView& v, hipStream_t st) {
-  if (debug_poison()) (void)hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st);
+  if (debug_poison()) qrk_chk(hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st));
 }
 constexpr int SPLIT_P = QRK_SPLIT > 1 ? QRK_SPLIT : 1;  // parts (1 when the split is off)
 template <int K>
@@ -2783,15 +2781,14 @@ void launch_xof_split(const RhoSrc& rs, size_t n, size_t C, const ScratchView& v
   int q0 = 0;
   if (QRK_SPLIT_LAG) {
     launch_xof<K>(rs.at(0), rs.stride, std::min(Cq, n), Cq, v, s.main, nullptr, 0);
-    (void)hipEventRecord(s.sub[0], s.main);
+    qrk_chk(hipEventRecord(s.sub[0], s.main));
     q0 = 1;
   }
-  (void)hipEventRecord(s.sfork, s.main);  // after the rho copy / part 0 / the previous chunk's cores
-  (void)hipStreamWaitEvent(s.side, s.sfork, 0);
+  fork_wait(s.main, s.side, s.sfork);  // after the rho copy / part 0 / the previous chunk's cores
   for (int q = q0; q < SPLIT_P; ++q) {
     const size_t off = (size_t)q * Cq, m = off < n ? std::min(Cq, n - off) : 0;
     if (m) launch_xof<K>(rs.at(off), rs.stride, m, Cq, v, s.side, nullptr, q);
-    (void)hipEventRecord(s.sub[q], s.side);
+    qrk_chk(hipEventRecord(s.sub[q], s.side));
   }
 }
 template <int K, int MODE>
@@ -2800,7 +2797,7 @@ void launch_core_split(size_t n, size_t C, const ScratchView& v, const Streams& 
                        const uint64_t* kbar, uint8_t* ss) {
   const size_t Cq = C / SPLIT_P;
   for (int q = 0; q < SPLIT_P; ++q) {
-    (void)hipStreamWaitEvent(s.main, s.sub[q], 0);
+    qrk_chk(hipStreamWaitEvent(s.main, s.sub[q], 0));
     const size_t off = (size_t)q * Cq;
     if (off >= n) continue;
     const size_t m = std::min(Cq, n - off);
@@ -2883,8 +2880,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const bool jside = QRK_J_SIDE && fs;
   poison_xof<K>(C, v, st);
   if (jside) {  // J(z || c) on the side stream, after this chunk's predecessors on main (kbar reuse)
-    (void)hipEventRecord(fs->fork, st);
-    (void)hipStreamWaitEvent(fs->side, fs->fork, 0);
+    fork_wait(st, fs->side, fs->fork);
     QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
   }
   if (split_ok<K>(n, C, s) && !jside) {

@@ -33,11 +33,36 @@ struct KernelTimer {
   virtual ~KernelTimer() = default;
 };
 extern thread_local KernelTimer* g_timer;
+// First kernel-launch error of the current library call (HIP resets its last-error state on every
+// later successful API call, so a failed launch followed by successful ones would otherwise go
+// unnoticed); run_batch clears it before each chunk and fails the call when it is set.
+extern thread_local hipError_t g_launch_err;
+
+// stream / event / memset calls inside the launchers: a failure joins g_launch_err
+inline void qrk_chk(hipError_t e) {
+  if (e != hipSuccess && g_launch_err == hipSuccess) g_launch_err = e;
+}
+
+// Order stream `to` after everything enqueued on the caller's stream `from` so far.  The host
+// waits for the event instead of hipStreamWaitEvent(to, ev): `from` may be the legacy NULL stream
+// (PyTorch's default), and a library stream made to wait on an event recorded there was observed
+// to run ahead -- the SampleNTT chain read keys the previous call had not finished writing
+// ("forks").  The host wait costs the pipelining of back-to-back calls, nothing else.
+inline void fork_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
+  (void)to;
+  qrk_chk(hipEventRecord(ev, from));
+  qrk_chk(hipEventSynchronize(ev));
+}
 
 #define QRK_LAUNCH(NAME, ST, ...)                   \
   do {                                              \
     if (::qrk::g_timer) ::qrk::g_timer->before(NAME, ST); \
     hipLaunchKernelGGL(__VA_ARGS__);                \
+    {                                               \
+      const hipError_t qrk_le_ = hipGetLastError(); \
+      if (qrk_le_ != hipSuccess && qrk_le_ != hipErrorNotReady && ::qrk::g_launch_err == hipSuccess) \
+        ::qrk::g_launch_err = qrk_le_;                \
+    }                                               \
     if (::qrk::g_timer) ::qrk::g_timer->after(NAME, ST);  \
   } while (0)
 

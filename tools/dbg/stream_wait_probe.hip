@@ -76,6 +76,29 @@ int main() {
   }
   for (int mode = 0; mode < 3; ++mode)
     printf("{\"A\": \"%s\", \"pipelined_misses\": %d, \"trials\": %d}\n", names[mode], pbad[mode], R);
+  // reverse direction: the producer is the NULL stream (the caller's stream under PyTorch), the
+  // waiter a non-blocking library stream (the launchers' forks), pipelined
+  {
+    int rbad = 0;
+    hipMemset(out, 0, 4096);
+    hipDeviceSynchronize();
+    hipEvent_t evs[R];
+    for (int r = 0; r < R; ++r) {
+      hipEventCreateWithFlags(&evs[r], hipEventDisableTiming);
+      busy_then_flag<<<256, 256, 0, 0>>>(flag, 900000 + r + 1, 2000000ull, sink);
+      hipEventRecord(evs[r], 0);
+      hipStreamWaitEvent(Anb, evs[r], 0);
+      read_flag<<<1, 64, 0, Anb>>>(flag, out, r);
+    }
+    hipDeviceSynchronize();
+    uint32_t h[R];
+    hipMemcpy(h, out, 4 * R, hipMemcpyDeviceToHost);
+    for (int r = 0; r < R; ++r) {
+      if (h[r] < 900000u + r + 1) ++rbad;
+      hipEventDestroy(evs[r]);
+    }
+    printf("{\"producer\": \"null\", \"waiter\": \"nonblocking\", \"pipelined_misses\": %d, \"trials\": %d}\n", rbad, R);
+  }
   for (int mode = 0; mode < 3; ++mode)
     printf("{\"A\": \"%s\", \"reused_event_misses\": %d, \"fresh_event_misses\": %d, \"trials\": %d}\n", names[mode],
            bad[mode][0], bad[mode][1], R);
