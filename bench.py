@@ -188,7 +188,9 @@ def kernel_ops_per_hs(alg, name, mode):
         perms = frodo_perms(alg)
         if name == "k_fr_gen_mm":  # Gen(A) Keccak (the bound) fused with S'A on MFMA
             return calls * perms["k_fr_gen_at"] * PERM_OPS, "valu"
-        if name == "k_fr_gen_mm_aes":  # Gen(A) AES-128 T-table lookups (LDS) fused with S'A on MFMA
+        if name in ("k_fr_gen_mm_aes", "k_fr_gen_mv_aes"):
+            # Gen(A) AES-128 T-table lookups (LDS) fused with S'A (on MFMA, or column-major on VALU
+            # in k_fr_gen_mv_aes): the same n * n/8 blocks either way
             return calls * n * (n // 8) * AES_LOOKUPS_PER_BLOCK, "lds"
         if name in ("k_fr_front_enc",):
             return (perms[name] * PERM_OPS if mode == "encdec" else None), "valu"
