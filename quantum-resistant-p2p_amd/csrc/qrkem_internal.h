@@ -48,10 +48,17 @@ inline void qrk_chk(hipError_t e) {
 // (PyTorch's default), and a library stream made to wait on an event recorded there was observed
 // to run ahead -- the SampleNTT chain read keys the previous call had not finished writing
 // ("forks").  The host wait costs the pipelining of back-to-back calls, nothing else.
+#ifndef QRK_FORK_HOST
+#define QRK_FORK_HOST 1
+#endif
 inline void fork_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
-  (void)to;
   qrk_chk(hipEventRecord(ev, from));
+#if QRK_FORK_HOST
+  (void)to;
   qrk_chk(hipEventSynchronize(ev));
+#else
+  qrk_chk(hipStreamWaitEvent(to, ev, 0));
+#endif
 }
 
 #define QRK_LAUNCH(NAME, ST, ...)                   \
