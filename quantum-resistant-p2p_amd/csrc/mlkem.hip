@@ -394,13 +394,44 @@ __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) 
 struct U3 {
   uint32_t x, y, z;
 };
-#if QRK_XOF_PACK12
-typedef U3 XUnit;
-#else
-typedef uint4 XUnit;
+// QRK_XOF_PAIR24 1 (with QRK_XOF_PACK12): tile units of two consecutive chunks (24 B) instead of
+// one, chunk pair p of entry i at ((i / TW) 16 + p) TW + i % TW -- a consumer lane's 16
+// coefficients are then 24 contiguous bytes (what the LDS-DMA prefetch needs, QRK_ENC_GLDS).
+#ifndef QRK_XOF_PAIR24
+#define QRK_XOF_PAIR24 QRK_ENC_GLDS
 #endif
+struct U6 {
+  U3 h[2];
+};
+#if QRK_XOF_PACK12
+typedef U3 XChunk;
+#if QRK_XOF_PAIR24
+typedef U6 XUnit;
+constexpr int XUNITS = 16;  // units per entry
+#else
+typedef U3 XUnit;
+constexpr int XUNITS = 32;
+#endif
+#else
+typedef uint4 XChunk;
+typedef uint4 XUnit;
+constexpr int XUNITS = 32;
+#endif
+// an entry's first unit, and chunk ch of it
+template <int TW>
+__device__ __forceinline__ XUnit* xent(XUnit* out, size_t inst) {
+  return out + (inst / TW) * XUNITS * TW + (inst % TW);
+}
+template <int TW>
+__device__ __forceinline__ XChunk* xc(XUnit* ent, int ch) {
+#if QRK_XOF_PACK12 && QRK_XOF_PAIR24
+  return &ent[(ch >> 1) * TW].h[ch & 1];
+#else
+  return ent + ch * TW;
+#endif
+}
 // r[j]: the chunk's coefficients (< 2^12, from the ring)
-__device__ __forceinline__ void chunk_store(XUnit* dst, const uint32_t r[8]) {
+__device__ __forceinline__ void chunk_store(XChunk* dst, const uint32_t r[8]) {
 #if QRK_XOF_PACK12
   U3 w;
   w.x = r[0] | (r[1] << 12) | (r[2] << 24);
@@ -414,7 +445,7 @@ __device__ __forceinline__ void chunk_store(XUnit* dst, const uint32_t r[8]) {
   *dst = make_uint4(w[0], w[1], w[2], w[3]);
 #endif
 }
-__device__ __forceinline__ void chunk_fill(XUnit* dst, uint32_t f) {  // timing probes only
+__device__ __forceinline__ void chunk_fill(XChunk* dst, uint32_t f) {  // timing probes only
 #if QRK_XOF_PACK12
   *dst = U3{f, f, f};
 #else
@@ -428,7 +459,7 @@ struct XofPend {
 template <int TW = 64>
 __device__ __forceinline__ void xof_pend_store(XofPend& pd, XUnit* dst) {
   if (pd.ch >= 0) {
-    chunk_store(dst + pd.ch * TW, pd.r);
+    chunk_store(xc<TW>(dst, pd.ch), pd.r);
     pd.ch = -1;
   }
 }
@@ -468,7 +499,7 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
       uint32_t w[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[j] = r[j * 128];
-      chunk_store(dst + ch * TW, w);
+      chunk_store(xc<TW>(dst, ch), w);
     }
   }
   cnt = (int)(P >> 9);
@@ -534,12 +565,12 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
       uint32_t w[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[j] = r[j * 64];
-      chunk_store(dst + ch * TW, w);
+      chunk_store(xc<TW>(dst, ch), w);
     }
 #endif
   }
 #if QRK_XOF_TIMING_ONLY >= 2
-  if (tsink == 0x12345678u) chunk_fill(dst, tsink);
+  if (tsink == 0x12345678u) chunk_fill(xc<TW>(dst, 0), tsink);
 #endif
 }
 
@@ -603,7 +634,7 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, XUnit* __restric
 #pragma unroll
       for (int e = 0; e < 8; ++e) cnt += c[e] < Q ? 1 : 0;
     }
-    chunk_fill(dst + b * TW, (uint32_t)cnt);
+    chunk_fill(xc<TW>(dst, b), (uint32_t)cnt);
     if (b == NB - 1) cnt = 256;
 #elif QRK_XOF_TIMING_ONLY == 1
     // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
@@ -611,7 +642,7 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, XUnit* __restric
     uint32_t f = 0;
 #pragma unroll
     for (int w = 0; w < 21; ++w) f ^= s.a[w].lo ^ s.a[w].hi;
-    chunk_fill(dst + b * TW, f);
+    chunk_fill(xc<TW>(dst, b), f);
     cnt = 256;
 #else
     compact_block<TW>(s, ring_all, rb, cnt, dst, pd);
@@ -631,7 +662,7 @@ __device__ __forceinline__ uint32_t* ring_entry(char* ring_all, uint32_t rb, int
 template <int K, bool ALL, int TW = 64>
 __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int xy, size_t inst, XUnit* __restrict__ out,
                                          char* ring_all, uint32_t rb) {
-  XUnit* dst = out + (inst / TW) * 32 * TW + (inst % TW);
+  XUnit* dst = xent<TW>(out, inst);
   KState s;
   xof_init(s, rho, xy, K);
   int cnt = 0;
@@ -662,7 +693,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
     KState s;
     xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
     int cnt = 0;
-    xof_blocks<false, 3, XTW>(s, cnt, out + (xwrap(inst) / XTW) * 32 * XTW + (xwrap(inst) % XTW), ring, rb);
+    xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(out, xwrap(inst)), ring, rb);
     if (cnt < 256) {
       const size_t slot = atomicAdd(nfix, 1u);
       if (slot < cap) {
@@ -697,7 +728,7 @@ __global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restr
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (base + j < cnt) *ring_entry(ring, rb, base + j) = rec[52 + j];
-        XUnit* dst = out + (inst / XTW) * 32 * XTW + (inst % XTW);
+        XUnit* dst = xent<XTW>(out, inst);
         xof_blocks<true, MAX_XOF_BLOCKS, XTW>(s, cnt, dst, ring, rb);
       } else {
         const size_t inst = fix[r - cap];
@@ -1455,8 +1486,13 @@ template <int TW = 64, bool P12 = false>
 __device__ __forceinline__ PK8 load_sampled(const void* __restrict__ xs_, size_t inst, int L) {
   if (TW == XTW) inst = xwrap(inst);
   if constexpr (P12) {
-    const U3* base = (const U3*)xs_ + (inst / TW) * 32 * TW + (inst % TW);
+    const XUnit* base = xent<TW>((XUnit*)xs_, inst);
+#if QRK_XOF_PAIR24
+    const U6 u = base[L * TW];
+    return unpack12(u.h[0], u.h[1]);
+#else
     return unpack12(base[(2 * L) * TW], base[(2 * L + 1) * TW]);
+#endif
   } else {
     const uint4* base = (const uint4*)xs_ + (inst / TW) * 32 * TW + (inst % TW);
     const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
@@ -1474,20 +1510,32 @@ __device__ __forceinline__ PK8 load_sampled(const void* __restrict__ xs_, size_t
 #ifndef QRK_ENC_GLDS
 #define QRK_ENC_GLDS 0
 #endif
-__device__ __forceinline__ void glds12(const void* gsrc, U3* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 12, 0, 0);
+// One lane's 24 contiguous bytes (a chunk pair, or 24 bytes of t_hat) global -> LDS as three
+// DMAs: 16 B into slab 0 (lane l at 16 l: the LDS destination of a DMA of S bytes is the wave base
+// + S l, and a 12-byte DMA also advances 16 B per lane, profiles/r3/glds12_layout_probe.txt), 4 B
+// into slab 1 and 4 B into slab 2 -- 1536 B per wave, no padding.  ab: the entry's 384 dwords.
+__device__ __forceinline__ void glds24(const void* gsrc, uint32_t* ab) {
+  const char* g = (const char*)gsrc;
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)ab, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 16),
+                                   (__attribute__((address_space(3))) void*)(ab + 256), 4, 0, 0);
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 20),
+                                   (__attribute__((address_space(3))) void*)(ab + 320), 4, 0, 0);
+}
+__device__ __forceinline__ void glds24_read(const uint32_t* ab, int wl, U3& lo, U3& hi) {
+  const uint4 a = ((const uint4*)ab)[wl];
+  lo = U3{a.x, a.y, a.z};
+  hi = U3{a.w, ab[256 + wl], ab[320 + wl]};
 }
 __device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // issue row `row`'s K entries (inst = (row K + j) Cx + hxs) into the wave's buffer
 template <int K>
-__device__ __forceinline__ void glds_row(const void* xof, size_t Cx, size_t hxs, int row, int L, U3* ab) {
+__device__ __forceinline__ void glds_row(const void* xof, size_t Cx, size_t hxs, int row, int L, uint32_t* ab) {
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const size_t inst = xwrap(((size_t)row * K + j) * Cx + hxs);
-    const U3* base = (const U3*)xof + (inst / XTW) * 32 * XTW + (inst % XTW);
-#pragma unroll
-    for (int c = 0; c < 2; ++c) glds12(base + (2 * L + c) * XTW, ab + (2 * j + c) * 64);
+    glds24(xent<XTW>((XUnit*)xof, inst) + L * XTW, ab + 384 * j);
   }
 }
 
@@ -1711,10 +1759,10 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
                                                       uint8_t* __restrict__ ct, int32_t* __restrict__ status,
                                                       const uint64_t* __restrict__ kprime,
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g,
-                                                      U3* ab = nullptr) {
+                                                      uint32_t* ab = nullptr) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   // ab: this wave's LDS prefetch buffer (QRK_ENC_GLDS; the batched kernel only)
-  constexpr bool GL = QRK_ENC_GLDS && QRK_XOF_PACK12 && QRK_ENC_PREFETCH && QRK_EK_PREFETCH && TW == 64;
+  constexpr bool GL = QRK_ENC_GLDS && QRK_XOF_PACK12 && QRK_XOF_PAIR24 && QRK_ENC_PREFETCH && QRK_EK_PREFETCH && TW == 64;
   const int wl = threadIdx.x & 63;
   (void)wl, (void)ab;
   const bool active = hs_raw < n;
@@ -1765,7 +1813,11 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     if constexpr (GL) {
       glds_wait();
 #pragma unroll
-      for (int j = 0; j < K; ++j) basemul_acc(acc, unpack12(ab[(2 * j) * 64 + wl], ab[(2 * j + 1) * 64 + wl]), yb[j]);
+      for (int j = 0; j < K; ++j) {
+        U3 lo, hi;
+        glds24_read(ab + 384 * j, wl, lo, hi);
+        basemul_acc(acc, unpack12(lo, hi), yb[j]);
+      }
     } else {
 #if QRK_ENC_PREFETCH
 #pragma unroll
@@ -1783,8 +1835,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
       } else if (LAST) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          glds12(ek + 384 * j + 24 * L, ab + (2 * j) * 64);
-          glds12(ek + 384 * j + 24 * L + 12, ab + (2 * j + 1) * 64);
+          glds24(ek + 384 * j + 24 * L, ab + 384 * j);
         }
       }
     } else {
@@ -1846,7 +1897,8 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
       uint32_t w[6];
       if constexpr (GL) {
         if (j == 0) glds_wait();
-        const U3 u = ab[(2 * j) * 64 + wl], v = ab[(2 * j + 1) * 64 + wl];
+        U3 u, v;
+        glds24_read(ab + 384 * j, wl, u, v);
         w[0] = u.x, w[1] = u.y, w[2] = u.z, w[3] = v.x, w[4] = v.y, w[5] = v.z;
       } else {
 #pragma unroll
@@ -1905,10 +1957,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? QR
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
 #if QRK_ENC_GLDS
-  __shared__ U3 abuf[4 * 2 * K * 64];
-  U3* ab = abuf + (threadIdx.x >> 6) * 2 * K * 64;
+  __shared__ uint32_t abuf[4 * 384 * K];
+  uint32_t* ab = abuf + (threadIdx.x >> 6) * 384 * K;
 #else
-  U3* ab = nullptr;
+  uint32_t* ab = nullptr;
 #endif
   encrypt_core_hs<K, MODE>(n, C, Cx, off, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
                            (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi], ab);
