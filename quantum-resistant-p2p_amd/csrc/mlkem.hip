@@ -396,9 +396,12 @@ struct U3 {
 };
 // QRK_XOF_PAIR24 1 (with QRK_XOF_PACK12): tile units of two consecutive chunks (24 B) instead of
 // one, chunk pair p of entry i at ((i / TW) 16 + p) TW + i % TW -- a consumer lane's 16
-// coefficients are then 24 contiguous bytes (what the LDS-DMA prefetch needs, QRK_ENC_GLDS).
+// coefficients are then 24 contiguous bytes (one load pair instead of two 12-byte loads 768 B
+// apart, and what the LDS-DMA prefetch needs).  A/B on one box, four interleaved pairs
+// (profiles/r3/final/ab_pair24.jsonl): encrypt core 1.97 -> 1.88 ms, fix-up 0.160 -> 0.103 ms per
+// 2^20 launch, k_xof unchanged.
 #ifndef QRK_XOF_PAIR24
-#define QRK_XOF_PAIR24 QRK_ENC_GLDS
+#define QRK_XOF_PAIR24 1
 #endif
 struct U6 {
   U3 h[2];
