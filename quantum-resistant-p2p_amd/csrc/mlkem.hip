@@ -2794,13 +2794,15 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
 #ifndef QRK_SPLIT
 #define QRK_SPLIT 0
 #endif
-// OFF by default: on three fresh boxes the back-to-back KeyGen -> Encaps sequence on one context
+// OFF by default.  With device-side forks (hipStreamWaitEvent on the caller's NULL-stream event),
+// on three fresh boxes the back-to-back KeyGen -> Encaps sequence on one context
 // (tests/test_gpu_split.py::test_split_back_to_back, the first GPU process on the box) returned
-// ciphertexts that differ from the serial schedule's in every row while the shared secrets matched,
-// i.e. the encrypt core read matrix entries the side stream had not yet written; warm reruns
-// (11 in one process, tools/dbg/split_loop.py) and an event-ordering probe of the same stream /
-// event pattern (tools/dbg/stream_wait_probe.hip, 0 misses in 360 waits) never showed it.  Until
-// the cause is found the pipeline is an A/B option (QRK_SPLIT=4: +2.9-3.6 % on the step).
+// ciphertexts that differ from the serial schedule's in every row while the shared secrets matched:
+// the side stream's SampleNTT parts ran on rho the caller's stream had not yet written.  Since the
+// forks are host-ordered (fork_wait) the same test passed as the first process on two fresh boxes,
+// with the matrix poisoned, plus the whole GPU suite on this variant (profiles/r3/split/) -- but
+// the host wait also takes away the pipelining the split lived on: +0.25 % (4 parts) and +0.0 %
+// (8 parts) against the unsplit schedule on one box, where it gained 2.9-3.6 % before.
 static_assert(QRK_SPLIT >= 0 && QRK_SPLIT <= 8, "QRK_SPLIT parts: one event and one spare fix-up counter each, 8 at most");
 #ifndef QRK_SPLIT_MIN
 #define QRK_SPLIT_MIN 262144
