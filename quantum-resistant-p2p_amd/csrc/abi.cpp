@@ -297,30 +297,6 @@ static size_t chunk_for(const qrk_ctx* ctx, const AlgInfo& a) {
   return cap;
 }
 
-// Per-chunk events of the ML-KEM split pipeline (Streams::sfork / sub): created before the chunk's
-// launches and released when the scope ends -- hipEventDestroy on an event whose work is still
-// pending releases it once the work completes -- so no event is re-recorded while an earlier
-// hipStreamWaitEvent on it may still be pending on the device.
-struct SplitEvents {
-  Streams& s;
-  bool on, ok = true;
-  SplitEvents(bool enable, Streams& st) : s(st), on(enable) {
-    if (!on) return;
-    ok = hipEventCreateWithFlags(&s.sfork, hipEventDisableTiming) == hipSuccess;
-    for (auto& ev : s.sub) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-  }
-  ~SplitEvents() {
-    if (!on) return;
-    if (s.sfork) (void)hipEventDestroy(s.sfork);
-    for (auto& ev : s.sub) {
-      if (ev) (void)hipEventDestroy(ev);
-      ev = nullptr;
-    }
-    s.sfork = nullptr;
-  }
-};
-
-
 // Routes QRK_LAUNCH timing to the context's timer for the scope's lifetime (nests).
 struct TimerScope {
   KernelTimer* prev;
@@ -342,12 +318,6 @@ struct CoinWipe {
     (void)hipMemsetAsync(ctx->dstage, 0, bytes, st);
   }
 };
-
-// QRK_FIX_SIDE 1: on the single-stream schedule the ML-KEM SampleNTT fix-up kernel (about one
-// wave per SIMD, latency-bound) runs on the side stream beside the front hash and PRFs
-#ifndef QRK_FIX_SIDE
-#define QRK_FIX_SIDE 1
-#endif
 
 // Core batched driver over device pointers, chunked.
 static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o1, uint8_t* o2, const uint8_t* i1,
@@ -395,9 +365,10 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   // chip and the overlap only stretches each kernel's span (profiles/r2/ab_streams*.json).
   const bool fork = ctx->streams == 2 || (ctx->streams == 0 && chunk < QRK_FORK_MAX);
   S.aux = fork ? ctx->aux : nullptr;
-  // streams == 1 is the documented serial schedule (kernel timings in isolation, qrkem.h): no
-  // side-stream fix-up there either
-  S.side = (QRK_FIX_SIDE && ctx->streams != 1) ? ctx->aux : nullptr;
+  // On the auto schedule the ML-KEM SampleNTT fix-up kernel (about one wave per SIMD, latency-bound)
+  // runs on the side stream beside the front hash and PRFs; streams == 1 is the documented serial
+  // schedule (kernel timings in isolation, qrkem.h): no side-stream fix-up there
+  S.side = ctx->streams != 1 ? ctx->aux : nullptr;
   S.fork = ctx->ev_fork;
   S.join = ctx->ev_join;
   if (ctx->flag_next) {
@@ -418,9 +389,6 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     hipError_t e = hipSuccess;
     g_launch_err = hipSuccess;
     (void)hipGetLastError();  // clear a stale error state (e.g. a caller's hipErrorNotReady query)
-    // fresh split-pipeline events for this chunk (ML-KEM Encaps / Decaps on the auto schedule)
-    SplitEvents split_ev(a.family == Family::MLKEM && op != Op::KEYPAIR && S.side && !S.aux && mlkem_split_parts(), S);
-    if (!split_ev.ok) return fail("cannot create split-pipeline events");
     if (a.family == Family::MLKEM) {
       switch (op) {
         case Op::KEYPAIR:

@@ -23,8 +23,9 @@
 //                                  Pack(B', C) staged in LDS; encaps: coalesced ct store;
 //                                  decaps: compare with ct, select k' or s (constant time)
 //   k_fr_ss           lane / hs   ss = H(ct || k)
-// KeyGen: k_fr_kg_front (seedA, SHAKE(0x5F || seedSE) stream), k_fr_sample,
-// k_fr_kg_rows (lane / row: Gen(A) row and B = AS + E on VALU), k_fr_kg_pack.
+// KeyGen: k_fr_kg_front (seedA, SHAKE(0x5F || seedSE) stream), k_fr_sample, B = AS + E fused with
+// Gen(A) (SHAKE: k_fr_kg_mm on i8 MFMA; AES: k_fr_kg_rows_aes, lane / row on VALU), k_fr_kg_pack.
+// AES Gen(A): k_fr_aes_prep + k_fr_gen_mv_aes (column-major, S'A on v_pk_mad_u16).
 #include "aes.cuh"
 #include "keccak.cuh"
 #include "keccak_coop.cuh"
@@ -37,12 +38,6 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr int NBAR = 8;
 // KeyGen B = AS + E for FrodoKEM-SHAKE: 1 = fused Gen(A) + i8 MFMA (k_fr_kg_mm), 0 = VALU rows
-#ifndef QRK_FR_KG_MM
-#define QRK_FR_KG_MM 1
-#endif
-#ifndef QRK_KG_ACC_VALU
-#define QRK_KG_ACC_VALU 0
-#endif
 constexpr int ST_PITCH = 72;  // LDS pitch (u16) of one column of a 64-row A block: 144 B -> conflict-free 16-B reads
 
 template <int N_>
@@ -235,14 +230,9 @@ __global__ __launch_bounds__(256) void k_fr_se_stream(const uint64_t* __restrict
   squeeze_tiled<P::RW>(s, raw, hs, W, RAWW);
 }
 
-// QRK_FR_SAMPLE_TILED 1: threads follow the tiled stream layout (coalesced reads, packed but
-// handshake-strided stores); 0 (default): one thread per (hs, word) in handshake order (strided
-// reads, stores contiguous across the wave).  A/B at FrodoKEM-640 2^16: 1.68-1.72 ms against
-// 1.40 ms (profiles/r2/ab_fr_sample_tiled_rejected.jsonl) -- the scattered stores cost more than
-// the scattered reads.
-#ifndef QRK_FR_SAMPLE_TILED
-#define QRK_FR_SAMPLE_TILED 0
-#endif
+// One thread per (hs, word) in handshake order: strided reads, stores contiguous across the wave
+// (following the tiled stream layout instead ran 1.68-1.72 against 1.40 ms at FrodoKEM-640 2^16,
+// profiles/r2/ab_fr_sample_tiled_rejected.jsonl: the scattered stores cost more than the reads).
 // CDF sampler over the raw stream.  Encaps (KG=false): words -> S' (8N, int8 [8][NP]),
 // E' (8N, int16 [8][N]), E'' (64).  KeyGen (KG=true): S^T (8N -> int8 [8][NP]) and E (8N, int16 [N][8]).
 template <int N, bool KG>
@@ -253,32 +243,6 @@ __global__ __launch_bounds__(256) void k_fr_sample(const uint64_t* __restrict__ 
   constexpr int NV = KG ? 2 * N * NBAR : (2 * N + NBAR) * NBAR;  // 16-bit samples per hs
   constexpr int NW = NV / 4;
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;  // one u64 = 4 samples
-#if QRK_FR_SAMPLE_TILED
-  // thread t reads raw[t]: the tiled stream [C/64][W][64] in order, so a wave's read is 512
-  // contiguous bytes (64 handshakes, one word each); the 4 samples of a word are consecutive
-  // entries of one output row and leave as one 4-byte (S') or 8-byte (E', E'') store
-  static_assert(N % 4 == 0 && NW * 4 == NV, "a word's 4 samples stay in one row");
-  const size_t hs = ((t >> 6) / (size_t)RAWW) * 64 + (t & 63);
-  const int w = (int)((t >> 6) % (size_t)RAWW);
-  if (hs >= n || w >= NW) return;
-  const uint64_t x = raw[t];
-  int v[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = cdf_sample<N>((uint32_t)(x >> (16 * e)) & 0xFFFF);
-  const int idx = 4 * w;
-  if (idx < NBAR * N) {
-    const int k = idx / N, j = idx % N;
-    *(uint32_t*)(sp8 + (hs * NBAR + k) * P::NP + j) =
-        (uint32_t)(uint8_t)v[0] | (uint32_t)(uint8_t)v[1] << 8 | (uint32_t)(uint8_t)v[2] << 16 | (uint32_t)(uint8_t)v[3] << 24;
-  } else {
-    const uint64_t q = (uint64_t)(uint16_t)v[0] | (uint64_t)(uint16_t)v[1] << 16 | (uint64_t)(uint16_t)v[2] << 32 |
-                       (uint64_t)(uint16_t)v[3] << 48;
-    if (idx < 2 * NBAR * N)
-      *(uint64_t*)(ep16 + hs * NBAR * N + (idx - NBAR * N)) = q;
-    else
-      *(uint64_t*)(epp16 + hs * 64 + (idx - 2 * NBAR * N)) = q;
-  }
-#else
   const size_t hs = t / NW;
   const int w = (int)(t % NW);
   if (hs >= n) return;
@@ -296,7 +260,6 @@ __global__ __launch_bounds__(256) void k_fr_sample(const uint64_t* __restrict__ 
       epp16[hs * 64 + (idx - 2 * NBAR * N)] = (int16_t)v;
     }
   }
-#endif
   // zero the K padding of S' rows once per hs (pad columns N..NP)
   if (w < NBAR && P::NP > N) {
     for (int j = N; j < P::NP; ++j) sp8[(hs * NBAR + w) * P::NP + j] = 0;
@@ -449,156 +412,6 @@ __global__ __launch_bounds__(256) void k_fr_aes_prep(const uint8_t* __restrict__
   u[3] = Tg(2, B(y1, 2)) ^ Tg(3, B(y2, 3)) ^ rk[11];
 }
 
-// Gen(A) with AES-128 fused with S'A on i8 MFMA.  Same contraction as k_fr_gen_mm (one
-// wave = 64 consecutive rows of one handshake, lane = row, per-wave u16 partial sums of
-// S'A), but the 512-thread workgroup's 8 waves share one LDS-replicated T-table, and A is
-// produced 16 columns (two interleaved AES blocks) per MFMA stage.
-#ifndef QRK_AES_WAVES
-#define QRK_AES_WAVES 16
-#endif
-#ifndef QRK_AES_COLS
-#define QRK_AES_COLS 16
-#endif
-#ifndef QRK_AES_T2
-#define QRK_AES_T2 1
-#endif
-#ifndef QRK_AES_BSTG
-#define QRK_AES_BSTG 1
-#endif
-constexpr int AES_WAVES = QRK_AES_WAVES;
-constexpr int AES_COLS = QRK_AES_COLS;
-template <int N>
-__global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t* __restrict__ prep, size_t n,
-                                                       const int8_t* __restrict__ sp8, uint16_t* __restrict__ part) {
-  using P = FP<N>;
-  static_assert(N % 16 == 0 && AES_COLS % 16 == 0, "MFMA stages assume whole 16-column tiles (block pairs)");
-#if QRK_AES_T2
-  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry
-  aes::fill_lds2(tab, threadIdx.x, 64 * AES_WAVES);
-#else
-  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
-  aes::fill_lds(tab, threadIdx.x, 64 * AES_WAVES);
-#endif
-#if QRK_AES_BSTG
-  // one byte per (column, row): lo limbs, MFMA, then hi limbs in the same 1 KiB, so 16 waves
-  // fit twice per CU beside the 64 KiB table (2 x 80 KiB)
-  __shared__ __attribute__((aligned(16))) uint8_t stb[AES_WAVES][16 * 64];
-#else
-  __shared__ __attribute__((aligned(16))) uint16_t stg[AES_WAVES][AES_COLS * ST_PITCH];
-#endif
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t item = (uint32_t)blockIdx.x * AES_WAVES + (uint32_t)wave;
-  if (item >= (uint32_t)(n * P::NWV)) return;
-  const uint32_t hs = __builtin_amdgcn_readfirstlane(item / P::NWV);
-  const int wv = (int)__builtin_amdgcn_readfirstlane(item % P::NWV);
-  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
-#if QRK_AES_T2
-  const aes::Lds2 L{(const char*)tab, (uint32_t)(lane & 31) * 4u, 128u + (uint32_t)(lane & 31) * 4u};
-#else
-  const aes::Lds L{(const char*)tab, (uint32_t)(lane & 31) * 4u};
-#endif
-  const int r = wv * 64 + lane;
-  const int kq = lane & 15, ks = 16 * (lane >> 4);
-  v4i y = {0, 0, 0, 0};
-  if (kq < NBAR) y = *(const v4i*)(sp8 + ((size_t)hs * NBAR + kq) * P::NP + wv * 64 + ks);  // zero past row N
-  uint32_t lp[4];
-  aes::row_part(L, hp, (uint32_t)r, lp);
-  uint16_t* prt = part + ((size_t)hs * P::NWV + wv) * NBAR * N;
-#if QRK_AES_BSTG
-  static_assert(AES_COLS == 16, "byte staging holds one 16-column tile");
-  uint8_t* sb = stb[wave];
-  auto wsync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-#pragma unroll 1
-  for (int c0 = 0; c0 < N; c0 += 16) {
-    const uint32_t* u = hp + aes::PREP_HDR + 4 * (c0 >> 3);
-    uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
-    uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
-    aes::rounds_3_10_x2(L, z, w, hp);
-    const v4i zr = {0, 0, 0, 0};
-    v4i d[2];
-#pragma unroll
-    for (int limb = 0; limb < 2; ++limb) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {  // word q = values 2q, 2q+1 (little-endian u16)
-        const uint32_t x = q < 4 ? z[q] : w[q - 4];
-        const uint32_t y8 = limb ? add80(x) >> 8 : x;  // lo = a & 0xFF, hi = (a + 128) >> 8
-        sb[(2 * q) * 64 + lane] = (uint8_t)y8;
-        sb[(2 * q + 1) * 64 + lane] = (uint8_t)(y8 >> 16);
-      }
-      wsync();
-      const v4i xv = *(const v4i*)(sb + kq * 64 + ks);  // rows ks .. ks+15 of column kq
-      d[limb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, y, zr, 0, 0, 0);
-      wsync();
-    }
-    const int cl = 4 * (lane >> 4);
-    if (kq < NBAR) {
-      uint32_t v[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)d[0][g] + ((uint32_t)d[1][g] << 8)) & 0xFFFFu;
-      *(uint2*)(prt + kq * N + c0 + cl) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
-    }
-  }
-#else
-  uint16_t* st = stg[wave];
-#pragma unroll 1
-  for (int c0 = 0; c0 < N; c0 += AES_COLS) {
-    const int nc = (N - c0) < AES_COLS ? (N - c0) : AES_COLS;
-#pragma unroll
-    for (int b = 0; b < AES_COLS / 8; b += 2) {  // pairs of AES blocks (N / 8 is even)
-      if (8 * b < nc) {
-        const uint32_t* u = hp + aes::PREP_HDR + 4 * ((c0 >> 3) + b);
-        uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
-        uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
-        aes::rounds_3_10_x2(L, z, w, hp);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {  // word q = values 2q, 2q+1 (little-endian u16)
-          const uint32_t x = q < 4 ? z[q] : w[q - 4];
-          const uint32_t al = __builtin_amdgcn_perm(add80(x), x, 0x07020500u);
-          st[(8 * b + 2 * q) * ST_PITCH + lane] = (uint16_t)al;
-          st[(8 * b + 2 * q + 1) * ST_PITCH + lane] = (uint16_t)(al >> 16);
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int t = 0; t < AES_COLS / 16; ++t) {
-      if (16 * t < nc) {
-        const uint16_t* src = st + (16 * t + kq) * ST_PITCH + ks;
-        const uint4 a0 = *(const uint4*)src;
-        const uint4 a1 = *(const uint4*)(src + 8);
-        const uint32_t w8[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-        v4i xl, xh;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          xl[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x06040200u);
-          xh[q] = (int)__builtin_amdgcn_perm(w8[2 * q + 1], w8[2 * q], 0x07050301u);
-        }
-        const v4i zr = {0, 0, 0, 0};
-        const v4i dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, y, zr, 0, 0, 0);
-        const v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, y, zr, 0, 0, 0);
-        const int cl = 16 * t + 4 * (lane >> 4);
-        if (kq < NBAR) {
-          uint32_t v[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) v[g] = ((uint32_t)dl[g] + ((uint32_t)dh[g] << 8)) & 0xFFFFu;
-          *(uint2*)(prt + kq * N + c0 + cl) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-#endif
-}
-
 // Gen(A) with AES-128 fused with S'A on the VALU, column-major: one lane owns column block jb (8
 // columns of A) of one handshake and walks the rows i of its row range, two AES blocks in flight;
 // after round 2 a block's state is rowpart(i) ^ colpart(jb) (aes.cuh), so the lane keeps its
@@ -606,14 +419,12 @@ __global__ __launch_bounds__(64 * AES_WAVES) void k_fr_gen_mm_aes(const uint32_t
 // (S'[2q][i] | S'[2q+1][i] << 16, k_fr_kg_spairs) as it goes.  Each A value is multiplied into
 // the 8 outputs B'[k][8 jb + c] with 4 v_pk_mad_u16 (mod 2^16 is all Encaps needs: q | 2^16), so
 // the lane ends with whole sums for its columns -- no LDS staging beside the T-table (the kernel is
-// bound by the table lookups on the CU's LDS, where k_fr_gen_mm_aes's MFMA staging added ~12 %
-// more LDS instructions, while the four SIMDs have VALU to spare), and no per-wave partial sums.
-// FR_MV_R<N> row ranges per column block keep every handshake's lanes whole waves (waves never span
+// bound by the table lookups on the CU's LDS, where an i8-MFMA variant's operand staging added
+// ~12 % more LDS instructions (rejected by A/B in round 3) while the four SIMDs have VALU to
+// spare), and no per-wave partial sums.
+// fr_mv_r<N>() row ranges per column block keep every handshake's lanes whole waves (waves never span
 // two handshakes, so round keys and S' pairs are scalar loads): 640: 80 x 4 = 320 lanes, 976: 122
 // (+ 6 idle) = 128, 1344: 168 x 8 = 1344.  Output: R partial sums [hs][R][8][N], added by k_fr_pack.
-#ifndef QRK_FR_MV_AES
-#define QRK_FR_MV_AES 1
-#endif
 template <int N>
 constexpr int fr_mv_r() { return N == 640 ? 4 : (N == 976 ? 1 : 8); }
 template <int N>
@@ -955,62 +766,6 @@ __global__ __launch_bounds__(256) void k_fr_kg_spairs(size_t n, const int8_t* __
   ((uint4*)spair)[hs * N + c] = o;
 }
 
-// B = A S + E (mod 2^16) on VALU: lane r generates row r of A (SHAKE128) and multiplies each
-// value into the 8 accumulators with 4 v_pk_mad_u16 against the uniform S-pair table.
-// KeyGen is not on the encaps/decaps timed path (twice per exchange in the handshake driver).
-template <int N>
-__global__ __launch_bounds__(128) void k_fr_kg_rows(const uint8_t* __restrict__ pk, size_t n,
-                                                    const uint32_t* __restrict__ spair,
-                                                    const int16_t* __restrict__ e16, uint16_t* __restrict__ bmat) {
-  using P = FP<N>;
-  constexpr int WGS_PER_HS = P::NP / 128;
-  const uint32_t hs = __builtin_amdgcn_readfirstlane(blockIdx.x / WGS_PER_HS);
-  if (hs >= n) return;
-  const int r = (int)(blockIdx.x % WGS_PER_HS) * 128 + threadIdx.x;
-  if (r >= N) return;
-  const uint8_t* sa = pk + (size_t)hs * P::PK;
-  uint64_t in[3];
-  {
-    const uint64_t s0 = ((const uint64_t*)sa)[0], s1 = ((const uint64_t*)sa)[1];
-    in[0] = (uint64_t)(r & 0xFFFF) | (s0 << 16);
-    in[1] = (s0 >> 48) | (s1 << 16);
-    in[2] = s1 >> 48;
-  }
-  KState s;
-  kzero(s);
-  absorb_short<21, 3>(s, in, 18);
-  u16x2 acc[4];
-  {
-    const uint4 e = *(const uint4*)(e16 + ((size_t)hs * N + r) * NBAR);  // E[r][0..7], int16 LE
-    acc[0] = __builtin_bit_cast(u16x2, e.x), acc[1] = __builtin_bit_cast(u16x2, e.y);
-    acc[2] = __builtin_bit_cast(u16x2, e.z), acc[3] = __builtin_bit_cast(u16x2, e.w);
-  }
-  const uint32_t* sp = spair + (size_t)hs * N * 4;
-#pragma unroll 1
-  for (int b = 0; b < P::A_BLOCKS; ++b) {
-    if (b) keccak_f(s);
-    const int c0 = 84 * b;
-#pragma unroll
-    for (int w = 0; w < 21; ++w) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = c0 + 4 * w + e;
-        if (c < N) {
-          const uint32_t x = (e < 2) ? s.a[w].lo : s.a[w].hi;
-          const u16x2 vv = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(x, x, (e & 1) ? 0x03020302u : 0x01000100u));
-          const uint32_t* s4 = sp + (size_t)c * 4;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[q] = vv * __builtin_bit_cast(u16x2, s4[q]) + acc[q];
-        }
-      }
-    }
-  }
-  const uint32_t m = P::QMASK | (P::QMASK << 16);
-  *(uint4*)(bmat + ((size_t)hs * N + r) * NBAR) =
-      make_uint4(__builtin_bit_cast(uint32_t, acc[0]) & m, __builtin_bit_cast(uint32_t, acc[1]) & m,
-                 __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
-}
-
 // KeyGen B = A S + E (mod 2^16), Gen(A) fused with the product on i8 MFMA (SHAKE128 A).
 // One wave owns 64 consecutive rows of one handshake (lane = row r squeezes row r of A).
 // Each SHAKE128 block's 84 columns go to LDS row-major, one byte per (row, column) and limb
@@ -1095,14 +850,8 @@ __global__ __launch_bounds__(64) void k_fr_kg_mm(const uint8_t* __restrict__ pk,
           xl[q] = *(const int*)(st[0] + off + 4 * q);
           xh[q] = *(const int*)(st[1] + off + 4 * q);
         }
-#if QRK_KG_ACC_VALU
-        const v4i zr = {0, 0, 0, 0};
-        acc[t][0] += __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, h ? y1 : y0, zr, 0, 0, 0);
-        acc[t][1] += __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, h ? y1 : y0, zr, 0, 0, 0);
-#else
         acc[t][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xl, h ? y1 : y0, acc[t][0], 0, 0, 0);
         acc[t][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(xh, h ? y1 : y0, acc[t][1], 0, 0, 0);
-#endif
       }
     }
   }
@@ -1131,7 +880,7 @@ template <int N>
 constexpr int kg_threads() { return ((N + kg_wgs<N>() - 1) / kg_wgs<N>() + 63) / 64 * 64; }
 
 // FrodoKEM-AES KeyGen rows: B = A S + E (mod 2^16), lane = row, A from AES-128 with the
-// two-table LDS layout of k_fr_gen_mm_aes (two blocks per iteration), S from the uniform
+// two-table LDS T-table layout (aes.cuh, two blocks per iteration), S from the uniform
 // pair table (scalar loads), 4 packed 16-bit multiply-adds per A value.  Not on the timed path
 // of encaps/decaps, but twice per exchange in the handshake driver.
 template <int N>
@@ -1178,104 +927,6 @@ __global__ __launch_bounds__(kg_threads<N>()) void k_fr_kg_rows_aes(const uint32
   *(uint4*)(bmat + ((size_t)hs * N + r) * NBAR) =
       make_uint4(__builtin_bit_cast(uint32_t, acc[0]) & m, __builtin_bit_cast(uint32_t, acc[1]) & m,
                  __builtin_bit_cast(uint32_t, acc[2]) & m, __builtin_bit_cast(uint32_t, acc[3]) & m);
-}
-
-// FrodoKEM-AES KeyGen B = A S + E (mod 2^16) with Gen(A) (AES-128, k_fr_gen_mm_aes's LDS T-table
-// and round-2 shortcut) fused with the product on i8 MFMA -- the KeyGen counterpart of the encaps
-// kernel (FrodoKEM-AES is the plugin default, key_exchange.py:319, and KeyGen runs twice
-// per exchange, messaging.py:590, 809).  One wave owns 64 consecutive rows of A (lane = row r); each
-// 16-column stage (two AES blocks) is split into balanced int8 limbs (lo = a & 0xFF, hi =
-// ((a + 128) >> 8) & 0xFF, a == 256 hi + lo mod 2^16), staged row-major, 16 bytes per row and limb
-// (one ds_write_b128 per lane), and contracted over the 16 columns:
-//   D(16 rows x 16) += X(16 rows x 32) . Y(32 x 16),  X[r][c] = limb(A[r][c0 + c]), Y[c][k] = S[c0 + c][k]
-// with v_mfma_i32_16x16x32_i8, K slices 16..31 zero (lanes 32-63 feed zero Y), four 16-row tiles x
-// two limbs = 8 MFMAs per stage, i32 accumulation over all N columns (|acc| <= N 128 12 < 2^31).
-// The VALU rows kernel spends 64 v_pk_mad_u16 per 16 columns on this product; here it is 8 byte
-// perms + 8 packed adds, 2 LDS writes, 8 LDS reads and 8 MFMAs.  A/B on one box (FrodoKEM-976-AES
-// handshake mode, profiles/r3/ab_frodo976aes_kg_mm_aes_rejected.jsonl): 69.4 ms per 2^16 KeyGen
-// against 67.5 ms for the VALU rows kernel -- the AES T-table lookups bound both kernels on the
-// CU's LDS, where the VALU multiply-adds run for free on the four SIMDs and the staging does not,
-// so 0 (the rows kernel) stays the default.
-#ifndef QRK_FR_KG_MM_AES
-#define QRK_FR_KG_MM_AES 0
-#endif
-typedef int v2i __attribute__((ext_vector_type(2)));
-template <int N>
-__global__ __launch_bounds__(64 * AES_WAVES) void k_fr_kg_mm_aes(const uint32_t* __restrict__ prep, size_t n,
-                                                                 const int8_t* __restrict__ sp8,
-                                                                 const int16_t* __restrict__ e16,
-                                                                 uint16_t* __restrict__ bmat) {
-  using P = FP<N>;
-  static_assert(N % 16 == 0, "16-column stages (AES block pairs)");
-  __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 64];  // T0 | T2 interleaved per entry
-  __shared__ __attribute__((aligned(16))) uint8_t stb[AES_WAVES][64 * 16];  // [row][16 columns], one limb
-  aes::fill_lds2(tab, threadIdx.x, 64 * AES_WAVES);
-  __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t item = (uint32_t)blockIdx.x * AES_WAVES + (uint32_t)wave;
-  if (item >= (uint32_t)(n * P::NWV)) return;
-  const uint32_t hs = __builtin_amdgcn_readfirstlane(item / P::NWV);
-  const int wv = (int)__builtin_amdgcn_readfirstlane(item % P::NWV);
-  const uint32_t* hp = prep + (size_t)hs * aes::prep_words<N>();
-  const aes::Lds2 L{(const char*)tab, (uint32_t)(lane & 31) * 4u, 128u + (uint32_t)(lane & 31) * 4u};
-  const int r = wv * 64 + lane;
-  const bool row_ok = r < N;
-  const int kq = lane & 15, kh = lane >> 4;  // MFMA fragment: row / column kq, K slice 8 kh .. 8 kh + 7
-  uint32_t lp[4];
-  aes::row_part(L, hp, (uint32_t)r, lp);
-  const int8_t* srow = sp8 + ((size_t)hs * NBAR + (kq & 7)) * P::NP;  // S^T row (kq & 7)
-  uint8_t* sb = stb[wave];
-  v4i acc[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = (v4i){0, 0, 0, 0};
-  auto wsync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-#pragma unroll 1
-  for (int c0 = 0; c0 < N; c0 += 16) {
-    // Y: S[c0 + 8 kh .. +7][kq & 7] on K slices 0, 1; zero on slices 2, 3 (lanes 32-63)
-    v2i y = {0, 0};
-    if (kh < 2) y = *(const v2i*)(srow + c0 + 8 * kh);
-    const uint32_t* u = hp + aes::PREP_HDR + 4 * (c0 >> 3);
-    uint32_t z[4] = {lp[0] ^ u[0], lp[1] ^ u[1], lp[2] ^ u[2], lp[3] ^ u[3]};
-    uint32_t w[4] = {lp[0] ^ u[4], lp[1] ^ u[5], lp[2] ^ u[6], lp[3] ^ u[7]};
-    aes::rounds_3_10_x2(L, z, w, hp);
-    const uint32_t x[8] = {z[0], z[1], z[2], z[3], w[0], w[1], w[2], w[3]};  // values 2q, 2q + 1 in x[q]
-#pragma unroll
-    for (int limb = 0; limb < 2; ++limb) {
-      uint32_t b[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {  // bytes of values 4d .. 4d + 3
-        const uint32_t a0 = limb ? add80(x[2 * d]) : x[2 * d], a1 = limb ? add80(x[2 * d + 1]) : x[2 * d + 1];
-        b[d] = row_ok ? __builtin_amdgcn_perm(a1, a0, limb ? 0x07050301u : 0x06040200u) : 0u;
-      }
-      *(uint4*)(sb + lane * 16) = make_uint4(b[0], b[1], b[2], b[3]);
-      wsync();
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const v2i xv = *(const v2i*)(sb + (16 * t + kq) * 16 + 8 * (kh & 1));
-        acc[t][limb] = __builtin_amdgcn_mfma_i32_16x16x32_i8(*(const long*)&xv, *(const long*)&y, acc[t][limb], 0, 0, 0);
-      }
-      wsync();
-    }
-  }
-  // D[m][k]: m = row 16 t + 4 (lane >> 4) + g, k = lane & 15
-  if (kq < NBAR) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int rr = wv * 64 + 16 * t + 4 * kh + g;
-        if (rr < N) {
-          const size_t o = ((size_t)hs * N + rr) * NBAR + kq;
-          const uint32_t v = (uint32_t)acc[t][0][g] + ((uint32_t)acc[t][1][g] << 8) + (uint32_t)(int)e16[o];
-          bmat[o] = (uint16_t)(v & P::QMASK);
-        }
-      }
-    }
-  }
 }
 
 // pk = seedA || Pack(B);  sk = s || pk || S^T (int16 LE) || pkh.  One 256-thread workgroup
@@ -1462,31 +1113,23 @@ void launch_ss(const uint8_t* ct, size_t n, const View<N>& v, uint8_t* ss, hipSt
     QRK_LAUNCH("k_fr_ss", st, k_fr_ss<N>, dim3(blocks_for(n)), dim3(256), 0, st, ct, n, v.kk, ss);
 }
 
-// partial sums of S'A per handshake that k_fr_pack adds: one per 64-row wave (MFMA kernels), or the
-// column-major AES kernel's row ranges
+// partial sums of S'A per handshake that k_fr_pack adds: one per 64-row wave (the SHAKE MFMA
+// kernel), or the column-major AES kernel's row ranges
 template <int N, bool AES>
-constexpr int fr_npart() { return (AES && QRK_FR_MV_AES) ? fr_mv_r<N>() : FP<N>::NWV; }
+constexpr int fr_npart() { return AES ? fr_mv_r<N>() : FP<N>::NWV; }
 
-// per-wave partial sums of S'A for every handshake of the chunk (Gen(A) fused)
+// partial sums of S'A for every handshake of the chunk (Gen(A) fused)
 template <int N, bool AES>
 void launch_sa(const View<N>& v, const uint8_t* seed_base, size_t seed_stride, size_t n, hipStream_t st) {
-  using P = FP<N>;
   if constexpr (AES) {
-    if (QRK_FR_MV_AES) {
-      uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
-      QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
-      QRK_LAUNCH("k_fr_aes_prep", st, (k_fr_aes_prep<N, true>), dim3(blocks_for(n * (N / 8 + N))), dim3(256), 0, st,
-                 seed_base, seed_stride, n, v.aesp);
-      QRK_LAUNCH("k_fr_gen_mv_aes", st, k_fr_gen_mv_aes<N>, dim3(blocks_for(n * fr_mv_lph<N>(), 1024)), dim3(1024), 0,
-                 st, v.aesp, n, spair, v.part);
-      return;
-    }
-    QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, seed_base,
-               seed_stride, n, v.aesp);
-    QRK_LAUNCH("k_fr_gen_mm_aes", st, k_fr_gen_mm_aes<N>, dim3(blocks_for(n * P::NWV, AES_WAVES)),
-               dim3(64 * AES_WAVES), 0, st, v.aesp, n, v.sp8, v.part);
+    uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
+    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
+    QRK_LAUNCH("k_fr_aes_prep", st, (k_fr_aes_prep<N, true>), dim3(blocks_for(n * (N / 8 + N))), dim3(256), 0, st,
+               seed_base, seed_stride, n, v.aesp);
+    QRK_LAUNCH("k_fr_gen_mv_aes", st, k_fr_gen_mv_aes<N>, dim3(blocks_for(n * fr_mv_lph<N>(), 1024)), dim3(1024), 0,
+               st, v.aesp, n, spair, v.part);
   } else {
-    QRK_LAUNCH("k_fr_gen_mm", st, k_fr_gen_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, seed_base,
+    QRK_LAUNCH("k_fr_gen_mm", st, k_fr_gen_mm<N>, dim3((unsigned)(n * FP<N>::NWV)), dim3(64), 0, st, seed_base,
                seed_stride, n, v.sp8, v.part);
   }
 }
@@ -1542,24 +1185,16 @@ hipError_t keypair_t(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, v
   // S^T -> sp8 ([8][NP] int8), E -> ep16 as [N][8]
   QRK_LAUNCH("k_fr_sample", st, (k_fr_sample<N, true>), dim3(blocks_for(round64(n) * (P::KG_WORDS))), dim3(256), 0, st,
              v.raw, n, P::KG_WORDS, v.sp8, v.ep16, v.epp16);
-  uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
-  if ((AES && !QRK_FR_KG_MM_AES) || (!AES && !QRK_FR_KG_MM))
-    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
   if constexpr (AES) {
+    uint32_t* spair = (uint32_t*)v.raw;  // the sampler stream is consumed by now
+    QRK_LAUNCH("k_fr_kg_spairs", st, k_fr_kg_spairs<N>, dim3(blocks_for(n * N)), dim3(256), 0, st, n, v.sp8, spair);
     QRK_LAUNCH("k_fr_aes_prep", st, k_fr_aes_prep<N>, dim3(blocks_for(n * (N / 8))), dim3(256), 0, st, pk,
                (size_t)P::PK, n, v.aesp);
-    if (QRK_FR_KG_MM_AES)
-      QRK_LAUNCH("k_fr_kg_mm_aes", st, k_fr_kg_mm_aes<N>, dim3(blocks_for(n * P::NWV, AES_WAVES)),
-                 dim3(64 * AES_WAVES), 0, st, v.aesp, n, v.sp8, v.ep16, v.part);
-    else
-      QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())),
-                 dim3(kg_threads<N>()), 0, st, v.aesp, n, spair, v.ep16, v.part);
-  } else if (QRK_FR_KG_MM) {
+    QRK_LAUNCH("k_fr_kg_rows_aes", st, k_fr_kg_rows_aes<N>, dim3((unsigned)(n * kg_wgs<N>())), dim3(kg_threads<N>()),
+               0, st, v.aesp, n, spair, v.ep16, v.part);
+  } else {
     QRK_LAUNCH("k_fr_kg_mm", st, k_fr_kg_mm<N>, dim3((unsigned)(n * P::NWV)), dim3(64), 0, st, pk, n, v.sp8, v.ep16,
                v.part);
-  } else {
-    QRK_LAUNCH("k_fr_kg_rows", st, k_fr_kg_rows<N>, dim3((unsigned)(n * (P::NP / 128))), dim3(128), 0, st, pk, n,
-               spair, v.ep16, v.part);
   }
   QRK_LAUNCH("k_fr_kg_pack", st, k_fr_kg_pack<N>, dim3((unsigned)n), dim3(256), 0, st, n, v.part, v.sp8, pk, sk);
   if (coop_path(n))

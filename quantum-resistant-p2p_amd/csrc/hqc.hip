@@ -66,37 +66,14 @@ struct Params {
 template <int L> struct HQ;
 // A/B on one box (2^16): HQC-128 (5, 128) for both beats (9, 64) + (5, 256); HQC-256 Encaps keeps
 // one position class (5, 384) while its Decaps gains from three (15, 128) (profiles/r1/ab_hqc_prod.txt)
-#ifndef QRK_HQC128_TPB
-#define QRK_HQC128_TPB 256
-#endif
-#if QRK_HQC128_TPB == 512
-template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 5, 128, 3, 256, 512> {};
-#else
 template <> struct HQ<128> : Params<17669, 46, 384, 66, 75, 75, 16, 15, 3, 5, 128, 5, 128, 256> {};
-#endif
 // Threads per handshake for HQC-192 / 256 (A/B on one box, profiles/r2/ab_hqc_tpb.jsonl): HQC-256
 // runs 512 (3 workgroups x 8 waves per CU under its 52 KB of LDS, against 3 x 6 at 384): enc+dec
 // 3.81e6 -> 4.18e6 /s; HQC-192 stays at 256 (384 / 512 with three-word windows: 8.4e6 -> 7.25e6;
 // 384 with five-word windows, 35.7 KB of LDS: 6.2e6),
 // and so does HQC-128 (512: 17.2e6 -> 15.0e6; it already holds the 32-wave limit at 256).
-#ifndef QRK_HQC192_TPB
-#define QRK_HQC192_TPB 256
-#endif
-#if QRK_HQC192_TPB == 512
-template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 3, 512, 512> {};
-#elif QRK_HQC192_TPB == 384
-template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 3, 384, 384> {};
-#else
 template <> struct HQ<192> : Params<35851, 56, 640, 100, 114, 114, 24, 16, 5, 9, 128, 5, 256, 256> {};
-#endif
-#ifndef QRK_HQC256_TPB
-#define QRK_HQC256_TPB 512
-#endif
-#if QRK_HQC256_TPB == 512
 template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 512, 512> {};
-#else
-template <> struct HQ<256> : Params<57637, 90, 640, 131, 149, 149, 32, 29, 5, 15, 128, 5, 384, 384> {};
-#endif
 
 // ---------------------------------------------------------------- GF(2^8) = F2[x]/(x^8+x^4+x^3+x^2+1)
 struct alignas(4) GfTabs {
@@ -496,15 +473,10 @@ __device__ __forceinline__ void supports_raw(const uint64_t* words, int weight, 
 // The first term: every s_j broadcast once (v_readlane) and compared with all lanes (a ballot per
 // register, masked to j > i, OR-ed into 64-bit lane masks); the chain: pointer jumping over
 // (replaced, next) words gathered with ds_bpermute, ceil(log2 w) rounds.
-// QRK_HQC_DEDUPE_ROT 1: the first term by lane rotations (63 rounds of ds_bpermute, no SGPR
-// round trips); 2: v_readlane broadcasts into per-lane VGPR accumulators (no ballots / SALU);
-// 0 (default): one v_readlane broadcast of s_j per j, ballot per register.  Variant 2 is also
-// slower (HQC-128 enc_mul 0.85 vs 0.77 ms, profiles/r2/ab_hqc_dedupe_vreg_rejected.jsonl).  A/B on one box
-// (profiles/r2/ab_hqc_dedupe_rot_rejected.jsonl): the rotations are slower (HQC-128 enc_mul 0.976
-// vs 0.766 ms) -- the permutes compete with the products for the CU's LDS.
-#ifndef QRK_HQC_DEDUPE_ROT
-#define QRK_HQC_DEDUPE_ROT 0
-#endif
+// One v_readlane broadcast of s_j per j and a ballot per register.  The first term by lane rotations
+// (63 rounds of ds_bpermute: HQC-128 enc_mul 0.976 vs 0.766 ms, profiles/r2/ab_hqc_dedupe_rot_rejected.jsonl
+// -- the permutes compete with the products for the CU's LDS) or by broadcasts into per-lane VGPR
+// accumulators (0.85 vs 0.77 ms, ab_hqc_dedupe_vreg_rejected.jsonl) was slower.
 template <int WT>
 __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
   constexpr int NE = (WT + 63) / 64;
@@ -515,74 +487,6 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
   uint32_t v[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
-#if QRK_HQC_DEDUPE_ROT == 1
-  // first term, all lanes at once: element (e, l) meets element (f, (l + d) mod 64) for every
-  // rotation d (one ds_bpermute per register and d, independent across d, no SGPR round trips);
-  // index 64 f + l' exceeds 64 e + l iff f > e, or f == e and l + d < 64 (no wrap).  Padding
-  // lanes hold 0xFFFFFFFF, never equal to a support (< n).
-  bool hit[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    hit[e] = false;
-#pragma unroll
-    for (int f = e + 1; f < NE; ++f) hit[e] = hit[e] || v[f] == v[e];  // d = 0
-  }
-  // rotations in batches of DB: every permute of a batch is issued before the first compare,
-  // so the LDS round trips overlap instead of costing one each
-  constexpr int DB = 8;
-#pragma unroll
-  for (int d0 = 1; d0 < 64; d0 += DB) {
-    uint32_t p[DB][NE];
-#pragma unroll
-    for (int k = 0; k < DB; ++k)
-#pragma unroll
-      for (int f = 0; f < NE; ++f)
-        if (d0 + k < 64) p[k][f] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * ((lane + d0 + k) & 63), (int)v[f]);
-    __builtin_amdgcn_sched_barrier(0);  // keep the batch's permutes ahead of its compares
-#pragma unroll
-    for (int k = 0; k < DB; ++k) {
-      if (d0 + k >= 64) continue;
-      const bool nowrap = lane < 64 - (d0 + k);
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        bool h = nowrap && p[k][e] == v[e];
-#pragma unroll
-        for (int f = e + 1; f < NE; ++f) h = h || p[k][f] == v[e];
-        hit[e] = hit[e] || h;
-      }
-    }
-  }
-  uint32_t x[NE];  // REP | next chain index (or NONE)
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const uint32_t i = 64 * e + lane;
-    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
-    x[e] = (hit[e] ? REP : 0u) | ptr;
-  }
-#elif QRK_HQC_DEDUPE_ROT == 2
-  // first term with per-lane accumulators in VGPRs: s_j broadcast by v_readlane, then
-  // hit |= ((v ^ s_j) - 1) & (lane - lim) -- bit 31 set iff v == s_j (both < 2^15) and i < j --
-  // four full-rate VALU ops per (j, register), no ballots and no SALU round trips
-  uint32_t hacc[NE] = {};
-#pragma unroll
-  for (int j = 1; j < WT; ++j) {
-    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      if (64 * e >= j) continue;  // no i < j in this register
-      const int lim = j - 64 * e;  // lanes below lim have i < j
-      const uint32_t eq = (v[e] ^ sj) - 1u;
-      hacc[e] |= lim >= 64 ? eq : (eq & (uint32_t)(lane - lim));
-    }
-  }
-  uint32_t x[NE];  // REP | next chain index (or NONE)
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const uint32_t i = 64 * e + lane;
-    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
-    x[e] = (hacc[e] & 0x80000000u) | ptr;  // REP is bit 31
-  }
-#else
   uint64_t dup[NE] = {};
 #pragma unroll
   for (int j = 1; j < WT; ++j) {
@@ -602,7 +506,6 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
     const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
     x[e] = ((dup[e] >> lane) & 1 ? REP : 0u) | ptr;
   }
-#endif
 #pragma unroll 1
   for (int r = 0; r < ROUNDS; ++r) {
     uint32_t y[NE];
@@ -626,131 +529,17 @@ __device__ __forceinline__ void dedupe_wave_cf(uint32_t* s) {
     if (64 * e + lane < WT) s[64 * e + lane] = (x[e] & REP) ? (uint32_t)(64 * e + lane) : v[e];
 }
 
-// QRK_HQC_DEDUPE_WG 1: the closed form's first term spread over all NWV waves of the workgroup
-// (wave w takes j = w mod NWV, its ballot masks OR-ed into DUP in LDS), the chain on wave 0 --
-// for Decaps' single dedupe, where the other waves would otherwise wait at the barrier.
-// DUP[2 NE] zeroed and s visible before the call; every thread of the workgroup calls it.
-// Off by default: shorter per-handshake latency, but throughput-neutral with 8 waves per SIMD
-// resident (profiles/r2/ab_hqc_dedupe_wg_rejected.jsonl).
-#ifndef QRK_HQC_DEDUPE_WG
-#define QRK_HQC_DEDUPE_WG 0
-#endif
-template <int WT, int NWV>
-__device__ __forceinline__ void dedupe_wg(uint32_t* s, uint32_t* DUP) {
-  constexpr int NE = (WT + 63) / 64;
-  constexpr uint32_t NONE = 0xFFFFu, REP = 0x80000000u;
-  constexpr int ROUNDS = 32 - __builtin_clz(WT - 1);
-  static_assert(NE <= 3 && WT > 1, "weight");
-  const int tq = hq_tid(), lane = tq & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tq >> 6);
-  uint32_t v[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
-  uint64_t dup[NE] = {};
-#pragma unroll
-  for (int j = 1; j < WT; ++j) {
-    if (j % NWV != wv) continue;  // wave-uniform
-    const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)v[j >> 6], j & 63);
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      if (64 * e >= j) continue;
-      uint64_t m = __ballot(v[e] == sj);
-      if (64 * e + 64 > j) m &= (1ull << (j - 64 * e)) - 1;
-      dup[e] |= m;
-    }
-  }
-  if (lane < 2 * NE) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      w = lane == 2 * e ? (uint32_t)dup[e] : w;
-      w = lane == 2 * e + 1 ? (uint32_t)(dup[e] >> 32) : w;
-    }
-    if (w) atomicOr(&DUP[lane], w);
-  }
-  __syncthreads();
-  if (wv != 0) return;
-  uint32_t x[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const uint32_t i = 64 * e + lane;
-    const uint32_t ptr = (v[e] > i && v[e] < (uint32_t)WT) ? v[e] : NONE;
-    const uint32_t dw = DUP[2 * e + (lane >> 5)];
-    x[e] = ((dw >> (lane & 31)) & 1 ? REP : 0u) | ptr;
-  }
-#pragma unroll 1
-  for (int r = 0; r < ROUNDS; ++r) {
-    uint32_t y[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const uint32_t p = x[e] & NONE;
-      const int src = 4 * (int)(p & 63);
-      uint32_t g = 0;
-#pragma unroll
-      for (int f = 0; f < NE; ++f) {
-        const uint32_t gf = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)x[f]);
-        g = (p >> 6) == (uint32_t)f ? gf : g;
-      }
-      y[e] = p == NONE ? x[e] : ((x[e] & REP) | g);
-    }
-#pragma unroll
-    for (int e = 0; e < NE; ++e) x[e] = y[e];
-  }
-#pragma unroll
-  for (int e = 0; e < NE; ++e)
-    if (64 * e + lane < WT) s[64 * e + lane] = (x[e] & REP) ? (uint32_t)(64 * e + lane) : v[e];
-}
-
-// The spec's loop itself on one wave: step i (w-2 .. 0) broadcasts s_i (v_readlane), compares it
-// with every current s_j (a ballot per register, masked to j > i) and replaces s_i by i on a hit
-// (a wave-uniform decision): w - 1 dependent steps.
-template <int WT>
-__device__ __forceinline__ void dedupe_wave_loop(uint32_t* s) {
-  constexpr int NE = (WT + 63) / 64;
-  static_assert(NE <= 3 && WT > 1, "weight");
-  const int lane = hq_tid() & 63;
-  uint32_t v[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) v[e] = (64 * e + lane < WT) ? s[64 * e + lane] : 0xFFFFFFFFu;
-#pragma unroll
-  for (int i = WT - 2; i >= 0; --i) {
-    const int ei = i >> 6, li = i & 63;
-    const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)v[ei], li);
-    uint64_t hit = 0;
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      if (64 * e + 63 <= i) continue;  // no j > i in this register
-      uint64_t m = __ballot(v[e] == si);
-      if (64 * e <= i) m &= ~0ull << (i - 64 * e + 1);
-      hit |= m;
-    }
-    if (hit) v[ei] = lane == li ? (uint32_t)i : v[ei];
-  }
-#pragma unroll
-  for (int e = 0; e < NE; ++e)
-    if (64 * e + lane < WT) s[64 * e + lane] = v[e];
-}
-
-// QRK_HQC_DEDUPE_CF: 1 closed form (default), 0 the serial loop.  A/B on one box
-// (profiles/r2/ab_hqc_dedupe_staging.jsonl): HQC-128 / 256 enc+dec 17.26e6 / 3.76e6 (closed form,
-// LDS staging) against 16.37e6 / 3.43e6 with round 1's workgroup-wide dedupe.
-#ifndef QRK_HQC_DEDUPE_CF
-#define QRK_HQC_DEDUPE_CF 1
-#endif
+// The closed form on one wave.  A/B on one box (profiles/r2/ab_hqc_dedupe_staging.jsonl): HQC-128 /
+// 256 enc+dec 17.26e6 / 3.76e6 (closed form, LDS staging) against 16.37e6 / 3.43e6 with round 1's
+// workgroup-wide dedupe; the spec's serial loop, a workgroup-wide first term and a first term by
+// lane rotations were slower or throughput-neutral (profiles/r2/ab_hqc_dedupe_*_rejected.jsonl).
 template <int WT>
 __device__ __forceinline__ void dedupe_wave(uint32_t* s) {
-#if QRK_HQC_DEDUPE_CF
   dedupe_wave_cf<WT>(s);
-#else
-  dedupe_wave_loop<WT>(s);
-#endif
 }
 
-// QRK_HQC_GDOUBLED: 1 the doubled operands are built straight from global words in the staging
-// phase (3 loads per word: 2-3 % slower); 0 raw words are staged in LDS first (default)
-#ifndef QRK_HQC_GDOUBLED
-#define QRK_HQC_GDOUBLED 0
-#endif
+// Raw words are staged in LDS first (building the doubled operands straight from global words, 3
+// loads per word, was 2-3 % slower).
 
 // doubled dense operand: D[q] = raw[q] ^ (clean << n)[q], raw words via rd(j) (0 outside [0, NW32)),
 // clean = raw masked to n bits.  Written for q in [0, NH2).
@@ -785,12 +574,9 @@ __device__ __forceinline__ void build_doubled(uint32_t* D, Rd rd) {
   }
 }
 
-// QRK_HQC_NOMB 1: both doubled operands built in place from raw words staged at the front of D1 / D2
+// Both doubled operands built in place from raw words staged at the front of D1 / D2
 // (every thread reads first, one barrier, then the stores), so enc_mul needs no separate staging /
 // message buffer and its LDS footprint drops by MBW words (more workgroups per CU for HQC-192/256).
-#ifndef QRK_HQC_NOMB
-#define QRK_HQC_NOMB 1
-#endif
 template <int L>
 __device__ __forceinline__ void build_doubled2_inplace(uint32_t* D1, uint32_t* D2) {
   using P = HQ<L>;
@@ -824,12 +610,8 @@ __device__ __forceinline__ void build_doubled2_inplace(uint32_t* D1, uint32_t* D
   }
 }
 
-// QRK_HQC_DPP_WIN 1: each window's last word from the neighbouring lane by DPP wave_shl:1 (one LDS
-// read fewer per window); A/B slower (HQC-128 enc_mul 0.818 vs 0.766 ms, HQC-256 6.18 vs 4.98 ms,
-// profiles/r2/ab_hqc_dpp_win_rejected.jsonl), off by default
-#ifndef QRK_HQC_DPP_WIN
-#define QRK_HQC_DPP_WIN 0
-#endif
+// (Taking each window's last word from the neighbouring lane by DPP wave_shl:1 was slower: HQC-128
+// enc_mul 0.818 vs 0.766 ms, HQC-256 6.18 vs 4.98 ms, profiles/r2/ab_hqc_dpp_win_rejected.jsonl.)
 // acc[c] ^= word (j0 + c) of X^k D-operand for the positions k of sup in this thread's class
 // (partial sums; prod_combine adds the classes)
 template <int L, int NV, int WPT, int NBT>
@@ -851,18 +633,8 @@ __device__ __forceinline__ void sparse_dense(const uint32_t* sup, int weight, co
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       uint32_t w[WPT + 1];
-#if QRK_HQC_DPP_WIN
-      // the window's last word is the next lane's first (a wave's lanes own consecutive
-      // windows at the same position): DPP wave_shl:1, one LDS read fewer per window; lane 63's
-      // neighbour is in the next wave, it reads its own
-#pragma unroll
-      for (int c = 0; c < WPT; ++c) w[c] = D[v][off + c];
-      w[WPT] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[0], 0x130, 0xF, 0xF, false);
-      if (lane63) w[WPT] = D[v][off + WPT];
-#else
 #pragma unroll
       for (int c = 0; c <= WPT; ++c) w[c] = D[v][off + c];
-#endif
 #pragma unroll
       for (int c = 0; c < WPT; ++c) acc[v][c] ^= alignbit(w[c + 1], w[c], sh);
     }
@@ -921,13 +693,8 @@ __device__ __forceinline__ void fill_gf(uint8_t* e, uint8_t* l) {
 }
 
 // ---------------------------------------------------------------- KeyGen: s = x + y h
-// QRK_HQC_KG_WPE: waves_per_eu pin for HQC-256's KeyGen product (0: unpinned, 107 VGPRs, 4 waves
-// per SIMD; 6: 76 VGPRs, no spill, 6 waves; 8 spills 92 B).  Not yet measured on the GPU: off.
-#ifndef QRK_HQC_KG_WPE
-#define QRK_HQC_KG_WPE 0
-#endif
 template <int L>
-__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 256 && QRK_HQC_KG_WPE ? QRK_HQC_KG_WPE : 1))) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(1))) void k_hqc_kg_mul(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ coins, uint8_t* __restrict__ pk,
                                                     uint8_t* __restrict__ sk) {
   using P = HQ<L>;
@@ -1000,32 +767,11 @@ __device__ unsigned long long g_hqc_trace[32];
 #endif
 
 // ---------------------------------------------------------------- Encaps / re-encryption
-// Persistent workgroups (QRK_HQC_PERSIST 1): a grid of a few workgroups per CU walks the
-// batch (hs = blockIdx.x, + gridDim.x, ...), and each iteration issues the NEXT handshake's global
-// reads (raw h and s words, supports, m) into
-// registers right after its own staging barrier; they land while this handshake's duplicate
-// removal, products and assembly run, taking the ~10 us load phase of a fresh workgroup
-// (profiles/r2/hqc128_phase_trace_*.json) off its critical path.  0 (default): one workgroup
-// per hs, the loop runs once.
-// A/B on one box (profiles/r2/ab_hqc_persist_rejected.jsonl): the persistent form is slower
-// (HQC-128 enc_mul 0.886 vs 0.761 ms, HQC-256 5.96 vs 4.94 ms): with 8 workgroups per CU the fresh
-// workgroups' load phases already overlap the resident ones' work, while the prefetch registers
-// cost spills or occupancy.  Kept as an option, off by default.
-#ifndef QRK_HQC_PERSIST
-#define QRK_HQC_PERSIST 0
-#endif
-#ifndef QRK_HQC_WPE
-#define QRK_HQC_WPE 8
-#endif
-#ifndef QRK_HQC_WPE192  // 72 VGPRs: 7 waves / SIMD, which the NOMB LDS footprint (21.5 KB) allows
-#define QRK_HQC_WPE192 7
-#endif
-#ifndef QRK_HQC_WPE256  // 64 VGPRs: 8 waves / SIMD = four 512-thread workgroups (37.6 KB LDS each)
-#define QRK_HQC_WPE256 8
-#endif
-#ifndef QRK_HQC_WG_PER_CU
-#define QRK_HQC_WG_PER_CU 8
-#endif
+// One workgroup per handshake.  (Persistent workgroups that prefetch the next handshake's global
+// reads were slower, HQC-128 enc_mul 0.886 vs 0.761 ms, profiles/r2/ab_hqc_persist_rejected.jsonl:
+// with 8 workgroups per CU the fresh workgroups' load phases already overlap the resident ones'
+// work.)  The handshake's global reads are issued before any of them is used (enc_issue), so
+// they are one round trip.
 
 // word j of a byte string at any alignment, split in two halves: issue() starts the one or two
 // aligned dword loads (no use of the data), finish() combines them -- ld32_masked across a gap
@@ -1087,7 +833,7 @@ __device__ __forceinline__ void enc_issue(EncIn<L, REENC>& in, size_t hs, const 
 // 8 waves per SIMD at HQC-128 as before the loop (<= 64 VGPRs; HQC-192/256 are held to 5 by their
 // LDS): without the bound the compiler keeps loop-invariant values live across the handshake loop
 template <int L, bool REENC>
-__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 128 ? QRK_HQC_WPE : (L == 192 ? QRK_HQC_WPE192 : QRK_HQC_WPE256)))) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 192 ? 7 : 8))) void k_hqc_enc_mul(size_t n, const uint64_t* __restrict__ row,
                                                      const uint8_t* __restrict__ coins, const uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ ct_out, const uint8_t* __restrict__ mp,
                                                      const uint8_t* __restrict__ sk, const uint8_t* __restrict__ ct_in,
@@ -1095,7 +841,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
   using P = HQ<L>;
   // NOMB: the message is assembled over u (D1) once u has been read out (HQC-128 is wave-limited,
   // not LDS-limited, and keeps the separate buffer: the in-place path costs it a spill at 64 VGPRs)
-  constexpr bool NOMB = QRK_HQC_NOMB && L != 128;
+  constexpr bool NOMB = L != 128;
   __shared__ __attribute__((aligned(16))) uint32_t D1[P::NH2];
   __shared__ uint32_t D2[P::NH2];
   __shared__ __attribute__((aligned(16))) uint32_t MBX[NOMB ? 4 : P::MBW];
@@ -1116,7 +862,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
   const int t0 = threadIdx.x;
   if (t0 < 128) ((uint32_t*)GE)[t0] = ((const uint32_t*)GF.exp)[t0];
   if (t0 < 64) ((uint32_t*)GL)[t0] = ((const uint32_t*)GF.log)[t0];
-  const size_t hstep = QRK_HQC_PERSIST ? gridDim.x : n;
+  const size_t hstep = n;  // one handshake per workgroup: the loop body runs once
   EncIn<L, REENC> in;
   enc_issue<L, REENC>(in, hs, row, coins, pk, mp, sk);
 #pragma unroll 1
@@ -1140,7 +886,6 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
     if (t == 0) DIFF = 0;
     __syncthreads();
     HQ_MARK(1 + 8 * REENC);
-    if (QRK_HQC_PERSIST && hs + hstep < n) enc_issue<L, REENC>(in, hs + hstep, row, coins, pk, mp, sk);
     // phase B: RS parity (wave 3), the three duplicate removals on waves 0-2
     if constexpr (NOMB) {
       build_doubled2_inplace<L>(D1, D2);
@@ -1312,30 +1057,18 @@ __device__ __forceinline__ uint32_t max_wave(uint32_t k) {
 }
 
 // ---------------------------------------------------------------- Decaps: m' = C.decode(v - u y)
-// QRK_HQC_DEC_ALIAS 1: the combined product T reuses the u || v staging buffer (v is folded into
-// the partial sums before the combine), one barrier more and NWP words less LDS per workgroup
-#ifndef QRK_HQC_DEC_ALIAS
-#define QRK_HQC_DEC_ALIAS 1
-#endif
-#ifndef QRK_HQC_DEC_WPE  // HQC-192 (56 VGPRs); HQC-128 / 256 fit 8 waves unconstrained (256 spills when pinned)
-#define QRK_HQC_DEC_WPE 8
-#endif
+// The combined product T reuses the u || v staging buffer (v is folded into the partial sums before
+// the combine): one barrier more and NWP words less LDS per workgroup
 template <int L>
-__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 192 ? QRK_HQC_DEC_WPE : 1))) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
+__global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L == 192 ? 8 : 1))) void k_hqc_decode(size_t n, const uint64_t* __restrict__ row,
                                                     const uint8_t* __restrict__ ct, uint8_t* __restrict__ syms,
                                                     size_t sym_stride) {
   using P = HQ<L>;
   __shared__ uint32_t D1[P::NH2];
   constexpr int MBD = (P::NB + P::VB + 8) / 4 + 1;
-#if QRK_HQC_DEC_ALIAS
   __shared__ uint32_t MB[MBD > P::NWP ? MBD : P::NWP];
   uint32_t* const T = MB;
-#else
-  __shared__ uint32_t T[P::NWP];
-  __shared__ uint32_t MB[MBD];
-#endif
   __shared__ uint32_t SY[P::WMAX];
-  __shared__ uint32_t DUP[6];
   __shared__ uint8_t SYM[128];
   const size_t hs = blockIdx.x;
   if (hs >= n) return;
@@ -1348,24 +1081,12 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
   // cut), u || v bytes staged, supports -- all of the handshake's global reads before the barrier
   constexpr int VALID = P::NB - 4 * (P::NW32 - 1);
   constexpr uint32_t BM = VALID >= 4 ? 0xFFFFFFFFu : ((1u << (8 * VALID)) - 1);
-#if QRK_HQC_GDOUBLED
-  build_doubled<L>(D1, [&](int j) {
-    const uint32_t w = ld32_masked(c, j, P::NB + P::VB);
-    return j == P::NW32 - 1 ? (w & BM) : w;
-  });
-#endif
   for (int j = t; j < (P::NB + P::VB + 3) / 4; j += P::TPB) MB[j] = ld32_masked(c, j, P::NB + P::VB);
   supports_raw<L>(rw + P::RWW, P::W, SY);
-  if (t < 6) DUP[t] = 0;
   __syncthreads();
-#if !QRK_HQC_GDOUBLED
   build_doubled<L>(D1, [&](int j) { return j == P::NW32 - 1 ? (MB[j] & BM) : MB[j]; });
-#endif
   HQ_MARK(17);
-  if (QRK_HQC_DEDUPE_WG)
-    dedupe_wg<P::W, P::TPB / 64>(SY, DUP);
-  else if (wave == 0)
-    dedupe_wave<P::W>(SY);
+  if (wave == 0) dedupe_wave<P::W>(SY);
   __syncthreads();
   HQ_MARK(18);
   uint32_t acc[1][P::WPT] = {};
@@ -1385,7 +1106,7 @@ __global__ __launch_bounds__(HQ<L>::TPB) __attribute__((amdgpu_waves_per_eu(L ==
 #pragma unroll
     for (int q = 0; q < P::WPT; ++q) acc[0][q] = j0 + q < P::VW32 ? acc[0][q] : 0u;
   }
-  if (QRK_HQC_DEC_ALIAS) __syncthreads();  // every v read done before T overwrites it
+  __syncthreads();  // every v read done before T overwrites it
   uint32_t* const outs[1] = {T};
   prod_combine<1, P::WPT, P::NBT>(outs, acc, [] {});
   HQ_MARK(20);
@@ -1583,22 +1304,6 @@ hipError_t supports_t(int kind, size_t n, const uint32_t* r, uint32_t* sup, hipS
 // ---------------------------------------------------------------- launchers
 inline unsigned blocks_for(size_t t) { return (unsigned)((t + 255) / 256); }
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-// grid of a persistent workgroup kernel: as many workgroups as are resident at once (the
-// occupancy query, capped at QRK_HQC_WG_PER_CU per CU), never more than one per handshake.  A
-// workgroup beyond the resident set would only start after a resident one had finished its
-// whole share, so the grid must not exceed it.
-template <typename Kern>
-unsigned wg_grid(size_t n, Kern kern, int tpb) {
-  if (!QRK_HQC_PERSIST) return (unsigned)n;
-  int dev = 0, cus = 256, per = QRK_HQC_WG_PER_CU;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, tpb, 0) == hipSuccess && occ > 0 && occ < per) per = occ;
-  const size_t cap = (size_t)cus * (size_t)per;
-  return (unsigned)(n < cap ? n : cap);
-}
-
 template <int L>
 void launch_enc_expand(const uint8_t* m, size_t m_stride, const uint8_t* pk, size_t pk_stride, const uint8_t* salt,
                        size_t salt_stride, size_t n, uint64_t* row, hipStream_t st) {
@@ -1662,8 +1367,7 @@ hipError_t encaps_t(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const
   using P = HQ<L>;
   View v = carve<L>(scratch, n);
   launch_enc_expand<L>(coins, (size_t)P::ENC, pk, (size_t)P::PK, coins + P::K, (size_t)P::ENC, n, v.row, st);
-  static const unsigned genc = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, false>, P::TPB);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)(n < genc ? n : genc)), dim3(P::TPB), 0, st, n, v.row, coins,
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, false>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row, coins,
              pk, ct, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (const uint8_t*)nullptr, (int32_t*)nullptr,
              v.msg);
   launch_hash<L>(v.msg, n, ss, st);
@@ -1688,8 +1392,7 @@ hipError_t decaps_t(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk,
              (size_t)P::MW * 8, v.mp);
   launch_enc_expand<L>(v.mp, (size_t)32, sk + SEED + P::K, (size_t)P::SK, ct + P::NB + P::VB, (size_t)P::CT, n, v.row,
                        st);
-  static const unsigned gre = wg_grid(SIZE_MAX, k_hqc_enc_mul<L, true>, P::TPB);
-  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)(n < gre ? n : gre)), dim3(P::TPB), 0, st, n, v.row,
+  QRK_LAUNCH("k_hqc_enc_mul", st, (k_hqc_enc_mul<L, true>), dim3((unsigned)n), dim3(P::TPB), 0, st, n, v.row,
              (const uint8_t*)nullptr, (const uint8_t*)nullptr, (uint8_t*)nullptr, v.mp, sk, ct, stp, v.msg);
   launch_hash<L>(v.msg, n, ss, st);
   return hipGetLastError();

@@ -8,7 +8,8 @@
 //   iota    : 2 v_xor
 // = 180 VALU instructions per round, 4320 per permutation, no moves; 58 of them (the rotations)
 // issue at half rate on gfx950, and so do the 64-bit shifts that could replace them
-// (tools/rot64_probe.hip).  Two rounds per loop iteration (QRK_KECCAK_UNROLL).
+// (tools/rot64_probe.hip).  Two rounds per loop iteration (45.3 against 44.2 Top/s at one,
+// profiles/r2/rot64_unroll_probe.json).
 // XOR3 is emitted through inline asm because hipcc (ROCm 7.2) splits
 // __builtin_amdgcn_bitop3_b32(...,0x96) back into two v_xor_b32.
 //
@@ -26,29 +27,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
-// a | b and a ^ (~b & c) pinned to full-rate encodings (the compiler would otherwise fold a
-// preceding shift into the half-rate v_lshl_or_b32, or split chi into v_bfi + v_xor)
-__device__ __forceinline__ uint32_t or32(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_or_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ uint32_t chi3(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd2" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
 
 struct u2 {
   uint32_t lo, hi;
 };
 
-// QRK_KECCAK_SHIFT64 1: a rotation is one 64-bit shift (v_lshlrev_b64 / v_lshrrev_b64 yields
-// one half of the result exactly) + one 32-bit shift + one OR for the other half, in place of
-// two half-rate v_alignbit_b32 (tools/rot64_probe.hip).
-#ifndef QRK_KECCAK_SHIFT64
-#define QRK_KECCAK_SHIFT64 0
-#endif
+// 64-bit rotation as two funnel shifts.  (One 64-bit shift + one 32-bit shift + OR is no cheaper:
+// the 64-bit shifts issue at half rate too, 38.7 against 44.1 Top/s, profiles/r2/rot64_probe.json.)
 
 template <int N>
 __device__ __forceinline__ u2 rol(u2 x) {
@@ -56,23 +41,11 @@ __device__ __forceinline__ u2 rol(u2 x) {
     return x;
   } else if constexpr (N == 32) {
     return {x.hi, x.lo};
-#if QRK_KECCAK_SHIFT64
-  } else if constexpr (N < 32) {
-    uint64_t t;
-    asm("v_lshlrev_b64 %0, %2, %1" : "=v"(t) : "v"(((uint64_t)x.hi << 32) | x.lo), "i"(N));
-    return {or32((uint32_t)t, x.hi >> (32 - N)), (uint32_t)(t >> 32)};
-  } else {
-    uint64_t t;
-    asm("v_lshrrev_b64 %0, %2, %1" : "=v"(t) : "v"(((uint64_t)x.hi << 32) | x.lo), "i"(64 - N));
-    return {(uint32_t)t, or32((uint32_t)(t >> 32), x.lo << (N - 32))};
-  }
-#else
   } else if constexpr (N < 32) {
     return {__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - N), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - N)};
   } else {
     return {__builtin_amdgcn_alignbit(x.hi, x.lo, 64 - N), __builtin_amdgcn_alignbit(x.lo, x.hi, 64 - N)};
   }
-#endif
 }
 
 __constant__ static const uint32_t KRC_LO[24] = {
@@ -97,11 +70,8 @@ __device__ __forceinline__ void kzero(KState& s) {
   for (int i = 0; i < 25; ++i) s.a[i] = {0u, 0u};
 }
 
-// QRK_KECCAK_UNROLL: rounds per loop iteration (1, 2, 3, 4, 6 ...; 24 = fully unrolled)
-#ifndef QRK_KECCAK_UNROLL
-#define QRK_KECCAK_UNROLL 2
-#endif
-template <int U = QRK_KECCAK_UNROLL>
+// U rounds per loop iteration (24 = fully unrolled)
+template <int U = 2>
 __device__ __forceinline__ void keccak_fu(KState& s) {
 #pragma unroll U
   for (int r = 0; r < 24; ++r) {
@@ -150,19 +120,14 @@ __device__ __forceinline__ void keccak_fu(KState& s) {
 #pragma unroll
       for (int x = 0; x < 5; ++x) {
         const u2 b0 = B[x + 5 * y], b1 = B[(x + 1) % 5 + 5 * y], b2 = B[(x + 2) % 5 + 5 * y];
-#if QRK_KECCAK_SHIFT64
-        s.a[x + 5 * y].lo = chi3(b0.lo, b1.lo, b2.lo);
-        s.a[x + 5 * y].hi = chi3(b0.hi, b1.hi, b2.hi);
-#else
         s.a[x + 5 * y].lo = b0.lo ^ (~b1.lo & b2.lo);
         s.a[x + 5 * y].hi = b0.hi ^ (~b1.hi & b2.hi);
-#endif
       }
     s.a[0].lo ^= KRC_LO[r];
     s.a[0].hi ^= KRC_HI[r];
   }
 }
-__device__ __forceinline__ void keccak_f(KState& s) { keccak_fu<QRK_KECCAK_UNROLL>(s); }
+__device__ __forceinline__ void keccak_f(KState& s) { keccak_fu<2>(s); }
 
 __device__ __forceinline__ void kxor(KState& s, int i, uint64_t w) {
   // i must be a compile-time constant after inlining
@@ -179,32 +144,12 @@ __device__ __forceinline__ uint64_t kword(const KState& s, int i) {
 // NW is a compile-time constant so every state index is static.
 // The next block's words are loaded into registers before the current block's
 // permutation runs, so global-load latency hides behind the 24 rounds.
-// QRK_ABSORB_PREFETCH 1 (default): the next block's words are loaded into registers before the
-// current block's permutation (2 RW VGPRs more); 0: each block's words are loaded when absorbed
-// (latency left to the other resident waves, fewer VGPRs -> higher occupancy).  A/B: no faster for
-// ML-KEM (127 -> 82 VGPRs, 4 -> 5 waves / SIMD), slower for the FrodoKEM H(pk) and ss kernels
-// (profiles/r2/ab_absorb_prefetch.jsonl).
-#ifndef QRK_ABSORB_PREFETCH
-#define QRK_ABSORB_PREFETCH 1
-#endif
+// (Loading each block's words only when absorbed -- fewer VGPRs, more waves -- was no faster for
+// ML-KEM and slower for the FrodoKEM H(pk) and ss kernels, profiles/r2/ab_absorb_prefetch.jsonl.)
 template <int RW, int NW, uint32_t DS, typename Loader>
 __device__ __forceinline__ void absorb_words(KState& s, Loader ld) {
   constexpr int NFULL = NW / RW;
   constexpr int TAIL = NW % RW;
-#if !QRK_ABSORB_PREFETCH
-#pragma unroll 1
-  for (int b = 0; b < NFULL; ++b) {
-#pragma unroll
-    for (int w = 0; w < RW; ++w) kxor(s, w, ld(b * RW + w));
-    keccak_f(s);
-  }
-#pragma unroll
-  for (int w = 0; w < TAIL; ++w) kxor(s, w, ld(NFULL * RW + w));
-  s.a[TAIL].lo ^= DS;
-  s.a[RW - 1].hi ^= 0x80000000u;
-  keccak_f(s);
-  return;
-#endif
   uint64_t nxt[RW];
 #pragma unroll
   for (int w = 0; w < RW; ++w) nxt[w] = (NFULL > 0 || w < TAIL) ? ld(w) : 0;

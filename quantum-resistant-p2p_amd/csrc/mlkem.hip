@@ -31,21 +31,13 @@
 namespace qrk {
 namespace mlkem {
 
-// canon_f: add q to negative residues with a sign mask (1) or let the compiler select (0)
-#ifndef QRK_CANON_MASK
-#define QRK_CANON_MASK 1
-#endif
-
 constexpr int Q = 3329;
 constexpr int QINV = 62209;  // q^-1 mod 2^16
-// QRK_XOF_PACK12 1: the batched SampleNTT output holds 12-bit coefficients (384 B per matrix
-// entry, 8 per 12-byte chunk) instead of int16 (512 B): the encrypt core waits on memory, not on
-// the VALU (SQ wait_any 0.28-0.35 after the round-3 arithmetic cut its VALU instructions 20 % with
-// no change in time), and the matrix is 58 % of its HBM reads.
-#ifndef QRK_XOF_PACK12
-#define QRK_XOF_PACK12 1
-#endif
-constexpr int XOF_W = QRK_XOF_PACK12 ? 48 : 64;  // u64 words per matrix entry in scratch
+// The batched SampleNTT output holds 12-bit coefficients (384 B per matrix entry, 8 per 12-byte
+// chunk) rather than int16 (512 B): the encrypt core waits on memory, not on the VALU (SQ wait_any
+// 0.28-0.35 after the round-3 arithmetic cut its VALU instructions 20 % with no change in time), and
+// the matrix is 58 % of its HBM reads.
+constexpr int XOF_W = 48;    // u64 words per matrix entry in scratch
 constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
 constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
 
@@ -135,55 +127,31 @@ __device__ __forceinline__ int canon(int a) {
 constexpr float QF = 3329.0f;
 constexpr float QINVF = 1.0f / 3329.0f;
 constexpr float MAGIC = 12582912.0f;
-// QRK_FMAMK 1: the closing p - t q as v_fmamk_f32 (literal -q) in place of the v_fmac_f32 the
-// compiler picks, which issues at ~0.65 of the full rate (profiles/r1/valu_peak_r1b.json: fmac
-// 40.4 T, fmaak 64.4 T lane-ops/s)
-#ifndef QRK_FMAMK
-#define QRK_FMAMK 0
-#endif
+// p - t q.  (Forcing v_fmamk_f32 with a literal -q through inline asm, in place of the v_fmac_f32
+// the compiler picks at ~0.65 of the full rate, made the cores 7-10 % slower: hazard s_nops and
+// lost v_pk_fma_f32 pairing, profiles/r3/ab_fmamk_rejected_and_wrap_probe.jsonl.)
 __device__ __forceinline__ float fms_q(float t, float p) {  // p - t q
-#if QRK_FMAMK
-  float r;
-  asm("v_fmamk_f32 %0, %1, 0xc5501000, %2" : "=v"(r) : "v"(t), "v"(p));
-  return r;
-#else
   return __builtin_fmaf(t, -QF, p);
-#endif
 }
-// QRK_MODMUL3 1: the modular product / reduction as three FMAs with MAGIC folded into the
-// constants (below); 0: the round-2 form (product, rounding FMA, MAGIC subtraction, FMA).
-#ifndef QRK_MODMUL3
-#define QRK_MODMUL3 1
-#endif
+// The modular product / reduction as three FMAs with MAGIC folded into the constants (below), where
+// the round-2 form spent a product, a rounding FMA, the MAGIC subtraction and an FMA.
 // MAGIC * q = 9987 * 2^22, exact in fp32
 constexpr float MQF = MAGIC * QF;
 // x mod q, centered: |result| <= 1665 for |x| < 2^24 (|x / q - rint| <= 1/2 + 3e-4)
 // Three-FMA form: k = x/q + MAGIC rounds to MAGIC + kint (the binade [2^23, 2^24) has ulp 1);
 // fma(k, -q, MAGIC q) = -q kint exactly (|q kint| < 2^24 for |x| <= 1.677e7); x + that is exact.
 __device__ __forceinline__ float reduce_f(float x) {
-#if QRK_MODMUL3
   const float k = __builtin_fmaf(x, QINVF, MAGIC);
   return x + __builtin_fmaf(k, -QF, MQF);
-#else
-  const float t = __builtin_fmaf(x, QINVF, MAGIC) - MAGIC;
-  return fms_q(t, x);
-#endif
 }
 // x * z mod q, centered, exact when |x * z| < 2^24 (for |z| <= 1664: |x| < 10082).
 // zq = fl(z / q).  Three FMAs: k = MAGIC + round(x zq) (|x zq - x z / q| < 3e-4, so the
 // result stays within q/2 + 1), n = -q round(.) exactly, then x z + n with one rounding of an
-// exact integer below 2^24.  The round-2 form (QRK_MODMUL3 0) spent a product, the MAGIC
+// exact integer below 2^24.  The round-2 form spent a product, the MAGIC
 // subtraction and a three-VGPR fmac (0.65 of the full rate, profiles/r1/valu_peak_r1b.json).
 __device__ __forceinline__ float modmul_f(float x, float z, float zq) {
-#if QRK_MODMUL3
   const float k = __builtin_fmaf(x, zq, MAGIC);
   return __builtin_fmaf(x, z, __builtin_fmaf(k, -QF, MQF));
-#else
-  (void)zq;
-  const float p = x * z;
-  const float t = __builtin_fmaf(p, QINVF, MAGIC) - MAGIC;
-  return fms_q(t, p);
-#endif
 }
 // The same product for lane-indexed twiddles (the NTT layers after the transpose, basemul gamma)
 // stays on the round-2 form: its single constant per twiddle holds fewer live registers than z
@@ -207,28 +175,17 @@ __device__ __forceinline__ uint32_t f2bits(float x) {  // low 16 bits = x as int
 // canonical [0, q) integer of an exact fp32 integer
 __device__ __forceinline__ int canon_f(float x) {
   const int r = f2i(reduce_f(x));
-#if QRK_CANON_MASK
   return r + (sign_mask(r) & Q);
-#else
-  return r + ((r >> 31) & Q);
-#endif
 }
 // basemul accumulator (|acc| < 2^31) -> centered residue: acc = hi 2^16 + lo with
 // 2^16 = -1044 (mod q), |hi * 1044 + lo| < 5.1e6 (exact), then one reduction
-// QRK_ACC2 1: with HI = MAGIC + hi and LO = MAGIC + lo as bit patterns (no MAGIC subtractions),
+// With HI = MAGIC + hi and LO = MAGIC + lo as bit patterns (no MAGIC subtractions),
 // fma(HI, -1044, 1043 MAGIC) = -MAGIC - 1044 hi is an exact integer below 2^24 (|hi| < 2^11) and
 // adding LO leaves lo - 1044 hi exactly: two full-rate ops where the round-2 form spent two
 // subtractions and a three-VGPR fmac.
-#ifndef QRK_ACC2
-#define QRK_ACC2 1
-#endif
 __device__ __forceinline__ float acc_to_f(int acc) {
-#if QRK_ACC2
   const float hi = __int_as_float(0x4B400000 + (acc >> 16)), lo = __int_as_float(0x4B400000 | (acc & 0xFFFF));
   return reduce_f(__builtin_fmaf(hi, -1044.0f, 1043.0f * MAGIC) + lo);
-#else
-  return reduce_f(__builtin_fmaf(i2f(acc >> 16), -1044.0f, i2f(acc & 0xFFFF)));
-#endif
 }
 
 // Compress_d(x) = round(2^d x / q) mod 2^d for x in [0, q): exact via 24-bit mulhi
@@ -242,19 +199,11 @@ __device__ __forceinline__ int compress(int x) {
 // round(x 2^d / q) mod 2^d (adding q to v adds 2^d).  Correct rounding: v 2^(d+1) is even and
 // (2k + 1) q odd, so v 2^d / q is at least 1 / (2q) = 1.5e-4 from every half-integer, and the
 // constant's relative error 2^-24 moves it by at most 2517 * 2^-24 < 1.5e-4 for
-// |v 2^d / q| <= 2517.  Two full-rate ops where canon_f + compress spent about twelve
-// (QRK_COMPRESS_F 0).
-#ifndef QRK_COMPRESS_F
-#define QRK_COMPRESS_F 1
-#endif
+// |v 2^d / q| <= 2517.  Two full-rate ops where canon_f + compress spent about twelve.
 template <int D>
 __device__ __forceinline__ int compress_f(float v) {
-#if QRK_COMPRESS_F
   constexpr float C = (float)((double)(1 << D) / 3329.0);
   return (int)(__float_as_uint(__builtin_fmaf(v, C, MAGIC)) & ((1u << D) - 1));
-#else
-  return compress<D>(canon_f(v));
-#endif
 }
 template <int D>
 __device__ __forceinline__ int decompress(int y) {
@@ -270,20 +219,10 @@ __device__ __forceinline__ size_t tidx(size_t inst, int w, int W) {
 
 // 16-lane group synchronisation: a group never spans two waves, so ordering
 // LDS traffic inside the wave is enough.
-#ifndef QRK_GSYNC_FENCE
-#define QRK_GSYNC_FENCE 1
-#endif
 __device__ __forceinline__ void gsync() {
-#if QRK_GSYNC_FENCE
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#else
-  // The LDS unit performs one wave's DS instructions in issue order, so a lane's read
-  // issued after another lane's write of the same wave observes it without waiting for
-  // the write to complete; the wave barrier keeps the compiler from reordering them.
-  __builtin_amdgcn_wave_barrier();
-#endif
 }
 
 // 8 consecutive 12-bit fields of the little-endian 96-bit string w0|w1|w2
@@ -309,60 +248,13 @@ __device__ __forceinline__ void split12(uint32_t w0, uint32_t w1, uint32_t w2, i
 // lane-interleaved (entry i of lane l at dword i*64 + l of the wave's ring), so
 // every lane always hits its own LDS bank: the random per-lane write offsets
 // never conflict.  Output: 256 int16 coefficients per entry in a 64-entry tiled
-// layout (chunk c of entry i at ((i/64)*32 + c)*64 + i%64, 16-byte units), so
-// the consumer reads them without any parsing.  inst = (x*K + y) * C + hs.
+// layout of 12-bit chunks (see XUnit below), so the consumer reads them without any
+// parsing.  inst = (x*K + y) * C + hs.
 constexpr int MAX_XOF_BLOCKS = 16;
 
-// Occupancy hints (waves per SIMD lower bound; tuning knobs)
-#ifndef QRK_WPE_CORE
-#define QRK_WPE_CORE 1
-#endif
-#ifndef QRK_WPE_FRONT
-#define QRK_WPE_FRONT 1
-#endif
-#ifndef QRK_WPE_XOF
-#define QRK_WPE_XOF 1
-#endif
-#define QRK_CORE_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_CORE)))
-// QRK_XOF_CMP 0 (sign-mask acceptance, three full-rate ops per candidate) measured no faster
-// than v_cmp + v_cndmask in k_xof (profiles/r2/ab_xof_signmask_rejected.jsonl)
-#ifndef QRK_XOF_CMP
-#define QRK_XOF_CMP 1
-#endif
-#ifndef QRK_XOF_TIMING_ONLY
-#define QRK_XOF_TIMING_ONLY 0
-#endif
-// QRK_TIMING_WRAP N > 0 (timing probe, wrong output, never a default build): k_xof stores and the
-// batched cores load SampleNTT entry inst at inst % N, so the sampled matrix never leaves the
-// caches (N = 4096: 2 MB) -- the step with and without Â's HBM round trip at matched work
-#ifndef QRK_TIMING_WRAP
-#define QRK_TIMING_WRAP 0
-#endif
-__host__ __device__ __forceinline__ size_t xwrap(size_t inst) { return QRK_TIMING_WRAP ? inst % QRK_TIMING_WRAP : inst; }
-// QRK_XOF_ACC 1: SampleNTT acceptance as a shifted difference (compact_block below); A/B on one
-// box no faster than v_cmp + v_cndmask (profiles/r2/ab_xof_acc_rejected.jsonl), kept as an option
-#ifndef QRK_XOF_ACC
-#define QRK_XOF_ACC 0
-#endif
-#ifndef QRK_ENC_PREFETCH
-#define QRK_ENC_PREFETCH 1
-#endif
-// QRK_EK_PREFETCH 1: the encrypt core loads t_hat (for v) during the last u-row into the
-// matrix prefetch registers, instead of when v's basemul needs it (SQ: the core waits on memory
-// 25-29 % of its wave time, profiles/r2/sq_mlkem768_b20_r2b.txt)
-#ifndef QRK_EK_PREFETCH
-#define QRK_EK_PREFETCH 1
-#endif
-// QRK_CT_PREFETCH 1: the decrypt core loads the ciphertext's next row one row ahead
-#ifndef QRK_CT_PREFETCH
-#define QRK_CT_PREFETCH 0
-#endif
-// QRK_DK_PREFETCH 1: the decrypt core issues s_hat_j's load before u_j's NTT
-#ifndef QRK_DK_PREFETCH
-#define QRK_DK_PREFETCH 1
-#endif
-#define QRK_XOF_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_XOF)))
-#define QRK_FRONT_ATTR __attribute__((amdgpu_waves_per_eu(QRK_WPE_FRONT)))
+// Rejected SampleNTT acceptance forms (A/B on one box, no faster than v_cmp + v_cndmask): a sign
+// mask (three full-rate ops, profiles/r2/ab_xof_signmask_rejected.jsonl) and a shifted difference
+// advancing the ring position by (c - q) >> 23 (profiles/r2/ab_xof_acc_rejected.jsonl).
 
 // (a & m) | b as one v_bitop3_b32 (truth table 0xEA): full rate on gfx950, where
 // v_and_or_b32 issues at half rate (profiles/r1/valu_peak_r1b.json)
@@ -371,55 +263,30 @@ __device__ __forceinline__ uint32_t and_or3(uint32_t a, uint32_t m, uint32_t b) 
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(a), "s"(m), "v"(b));
   return r;
 }
-// (a << s) | b as one v_lshl_or_b32
-__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
-  uint32_t r;
-  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(s), "v"(b));
-  return r;
-}
 
 // Compact one squeezed SHAKE128 block (112 candidates) into the lane's ring,
 // flushing completed 8-coefficient chunks to dst.
 // `rb` = byte offset of the lane's ring column inside ring_all (wave * 4096 + lane * 4): bits
 // 8-11 are zero, so an entry address is one v_bitop3_b32, (pos & 0xF00) | rb, with the static
 // LDS base folded into the ds_write offset.
-// QRK_XOF_PIPE 1: a completed chunk's 8 ring entries are read when it completes and packed +
-// stored one triplet later (or after the block), so the LDS read latency is not waited for
-// on the spot
-#ifndef QRK_XOF_PIPE
-#define QRK_XOF_PIPE 1
-#endif
-// One 8-coefficient chunk of the batched SampleNTT output: 16 bytes of int16, or 12 bytes of
-// 12-bit fields (QRK_XOF_PACK12); chunk c of entry i at ((i / TW) 32 + c) TW + i % TW units.
+// A completed chunk's 8 ring entries are read when it completes and packed + stored one triplet
+// later (or after the block), so the LDS read latency is not waited for on the spot (-1.5 %,
+// profiles/r2/ab_xof_pipe_flush.jsonl).
+// One 8-coefficient chunk of the batched SampleNTT output: 12 bytes of 12-bit fields.
 struct U3 {
   uint32_t x, y, z;
 };
-// QRK_XOF_PAIR24 1 (with QRK_XOF_PACK12): tile units of two consecutive chunks (24 B) instead of
-// one, chunk pair p of entry i at ((i / TW) 16 + p) TW + i % TW -- a consumer lane's 16
-// coefficients are then 24 contiguous bytes (one load pair instead of two 12-byte loads 768 B
-// apart, and what the LDS-DMA prefetch needs).  A/B on one box, four interleaved pairs
+// Tile units of two consecutive chunks (24 B): chunk pair p of entry i at ((i / TW) 16 + p) TW +
+// i % TW, so a consumer lane's 16 coefficients are 24 contiguous bytes (one load pair instead of
+// two 12-byte loads 768 B apart).  A/B on one box, four interleaved pairs
 // (profiles/r3/final/ab_pair24.jsonl): encrypt core 1.97 -> 1.88 ms, fix-up 0.160 -> 0.103 ms per
 // 2^20 launch, k_xof unchanged.
-#ifndef QRK_XOF_PAIR24
-#define QRK_XOF_PAIR24 1
-#endif
 struct U6 {
   U3 h[2];
 };
-#if QRK_XOF_PACK12
 typedef U3 XChunk;
-#if QRK_XOF_PAIR24
 typedef U6 XUnit;
 constexpr int XUNITS = 16;  // units per entry
-#else
-typedef U3 XUnit;
-constexpr int XUNITS = 32;
-#endif
-#else
-typedef uint4 XChunk;
-typedef uint4 XUnit;
-constexpr int XUNITS = 32;
-#endif
 // an entry's first unit, and chunk ch of it
 template <int TW>
 __device__ __forceinline__ XUnit* xent(XUnit* out, size_t inst) {
@@ -427,33 +294,15 @@ __device__ __forceinline__ XUnit* xent(XUnit* out, size_t inst) {
 }
 template <int TW>
 __device__ __forceinline__ XChunk* xc(XUnit* ent, int ch) {
-#if QRK_XOF_PACK12 && QRK_XOF_PAIR24
   return &ent[(ch >> 1) * TW].h[ch & 1];
-#else
-  return ent + ch * TW;
-#endif
 }
 // r[j]: the chunk's coefficients (< 2^12, from the ring)
 __device__ __forceinline__ void chunk_store(XChunk* dst, const uint32_t r[8]) {
-#if QRK_XOF_PACK12
   U3 w;
   w.x = r[0] | (r[1] << 12) | (r[2] << 24);
   w.y = (r[2] >> 8) | (r[3] << 4) | (r[4] << 16) | (r[5] << 28);
   w.z = (r[5] >> 4) | (r[6] << 8) | (r[7] << 20);
   *dst = w;
-#else
-  uint32_t w[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) w[j] = lshl_or(r[2 * j + 1], 16, r[2 * j]);
-  *dst = make_uint4(w[0], w[1], w[2], w[3]);
-#endif
-}
-__device__ __forceinline__ void chunk_fill(XChunk* dst, uint32_t f) {  // timing probes only
-#if QRK_XOF_PACK12
-  *dst = U3{f, f, f};
-#else
-  *dst = make_uint4(f, f, f, f);
-#endif
 }
 struct XofPend {
   uint32_t r[8];  // the chunk's ring entries, in order
@@ -467,54 +316,10 @@ __device__ __forceinline__ void xof_pend_store(XofPend& pd, XUnit* dst) {
   }
 }
 
-#if QRK_XOF_ACC
-// Ring layout with a 512-B entry stride: the two waves of a pair interleave their 256-B entry
-// rows (wave & 1 selects the half), so the ring is still 16 KB per 4-wave workgroup.  The
-// running position is kept as P = 511 (cnt + 1): an accepted candidate adds
-// (uint)(c - q) >> 23 = 511 (c < q) or 0 (c >= q) -- two full-rate ops in place of the
-// v_cmp + v_cndmask pair (about three issue slots, profiles/r1/valu_peak_r1b.json) -- and
-// P >> 9 = cnt for every cnt <= 511, so bits 9-12 of P index the ring entry directly.
-template <int TW = 64>
-__device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, XUnit* dst,
-                                              XofPend&) {
-  const uint32_t* ring = (const uint32_t*)(ring_all + rb);
-  uint32_t P = 511u * (uint32_t)(cnt + 1);
-#pragma unroll
-  for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
-    uint32_t d[3];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const int di = 3 * t + e;
-      d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
-    }
-    int c[8];
-    split12(d[0], d[1], d[2], c);
-    const int before = (int)(P >> 9);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      *(uint32_t*)(ring_all + and_or3(P, 0x1E00u, rb)) = (uint32_t)c[e];
-      P += (uint32_t)(c[e] - Q) >> 23;
-    }
-    const int now = (int)(P >> 9);
-    const int ch = before >> 3;
-    if ((now >> 3) != ch && ch < 32) {
-      const uint32_t* r = ring + (ch & 1) * 8 * 128;
-      uint32_t w[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) w[j] = r[j * 128];
-      chunk_store(xc<TW>(dst, ch), w);
-    }
-  }
-  cnt = (int)(P >> 9);
-}
-#else
 template <int TW = 64>
 __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, uint32_t rb, int& cnt, XUnit* dst,
                                               XofPend& pd) {
   const uint32_t* ring = (const uint32_t*)(ring_all + rb);
-#if QRK_XOF_TIMING_ONLY >= 2
-  uint32_t tsink = 0;
-#endif
 #pragma unroll
   for (int t = 0; t < 14; ++t) {  // 42 dwords = 14 triplets of 8 twelve-bit candidates
     uint32_t d[3];
@@ -531,23 +336,11 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
     int pos = cnt << 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-#if QRK_XOF_TIMING_ONLY == 3
-      tsink ^= and_or3(pos, 0xF00u, rb) + (uint32_t)c[e];  // timing probe: no LDS write
-#else
       *(uint32_t*)(ring_all + and_or3(pos, 0xF00u, rb)) = (uint32_t)c[e];
-#endif
-#if QRK_XOF_CMP
       pos += c[e] < Q ? 256 : 0;
-#else
-      // accept iff c < q: the sign of c - q, as an all-ones / zero mask, selects the 256-B
-      // ring step -- three full-rate ops in place of v_cmp + v_cndmask, whose VCC round trip
-      // issues at a fraction of the VALU rate (profiles/r1/valu_peak_r1b.json)
-      pos += sign_mask(c[e] - Q) & 256;
-#endif
     }
     cnt = pos >> 8;
     const int ch = before >> 3;
-#if QRK_XOF_PIPE
     // the chunk completed one triplet ago: its ring reads were issued then, so they have
     // landed by now (a wave's LDS instructions execute in issue order, so the reads saw the
     // chunk before this triplet's writes could reuse its slots)
@@ -558,53 +351,17 @@ __device__ __forceinline__ void compact_block(const KState& s, char* ring_all, u
       for (int j = 0; j < 8; ++j) pd.r[j] = r[j * 64];
       pd.ch = ch;
     }
-#else
-#if QRK_XOF_TIMING_ONLY >= 2
-    if (false) {  // timing probe: no flush
-#else
-    if ((cnt >> 3) != ch && ch < 32) {
-#endif
-      const uint32_t* r = ring + (ch & 1) * 8 * 64;
-      uint32_t w[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) w[j] = r[j * 64];
-      chunk_store(xc<TW>(dst, ch), w);
-    }
-#endif
   }
-#if QRK_XOF_TIMING_ONLY >= 2
-  if (tsink == 0x12345678u) chunk_fill(xc<TW>(dst, 0), tsink);
-#endif
 }
 
-#endif
 
-// QRK_XOF_RESUME 1: an entry that still lacks values after its 3 blocks saves its
-// sponge state, count and partial chunk (a 256-B record), and the fix-up resumes from there --
-// usually one more permutation -- instead of recomputing the entry from scratch (4+ sequential
-// permutations on a lane that is nearly alone on its SIMD).  Records are reserved for K^2 C / 16
-// entries (about 9x the expected 0.7 %); entries beyond that (e.g. a batch of keys chosen for
-// bad rho) go to the from-scratch list.  A/B on one box (profiles/r2/ab_xof_resume.jsonl): the
-// fix-up drops from 0.35 to 0.25 ms and stops slowing the front / decrypt kernels it overlaps,
-// but k_xof itself runs 1.8 % slower with the record path compiled in -- no net gain, so 0 is
-// the default (every fix-up entry recomputed from scratch, cap = 0).
-#ifndef QRK_XOF_RESUME
-#define QRK_XOF_RESUME 0
-#endif
-#if QRK_XOF_RESUME && QRK_XOF_ACC
-#error "QRK_XOF_RESUME restores the ring layout of the default compaction (QRK_XOF_ACC=0)"
-#endif
-// QRK_XOF_TW: tile width of the batched SampleNTT output (chunk c of entry i at
-// ((i / XTW) 32 + c) XTW + i % XTW, 16-byte units): 64 (default) makes k_xof's stores one
-// contiguous KB per wave; 1 makes each entry's 512 B contiguous for the cores' 16-lane reads.
-// A/B (profiles/r2/ab_xof_tile_width.jsonl): 1 speeds the encrypt core up 4 % but slows k_xof's
-// scattered 16-byte stores 4-8 % (net -2 %); 8 is even with 64.
-#ifndef QRK_XOF_TW
-#define QRK_XOF_TW 64
-#endif
-constexpr int XTW = QRK_XOF_TW;
-constexpr int XOF_REC_WORDS = 64;  // [0] inst, [1] count, [2..51] state (lo, hi), [52..59] partial chunk
-__host__ __device__ inline size_t xof_rec_cap(int K, size_t C) { return (size_t)K * K * C / 16; }
+// Fix-up entries are recomputed from scratch.  (Resume records -- the sponge state, count and
+// partial chunk saved after the 3rd block, so the fix-up needs one more permutation -- cut the
+// fix-up from 0.35 to 0.25 ms but slowed k_xof 1.8 %: no net gain, profiles/r2/ab_xof_resume.jsonl.)
+// Tile width 64 makes k_xof's stores one contiguous KB per wave; width 1 (each entry contiguous)
+// sped the encrypt core up 4 % but slowed k_xof's scattered stores 4-8 % (net -2 %,
+// profiles/r2/ab_xof_tile_width.jsonl).
+constexpr int XTW = 64;
 
 __device__ __forceinline__ void xof_init(KState& s, const uint64_t* __restrict__ rho, int xy, int K) {
   kzero(s);
@@ -621,42 +378,9 @@ __device__ __forceinline__ void xof_blocks(KState& s, int& cnt, XUnit* __restric
 #pragma unroll 1
   for (int b = 0; b < NB && (!ALL || cnt < 256); ++b) {
     keccak_f(s);
-#if QRK_XOF_TIMING_ONLY == 4
-    // timing probe: the permutations plus the acceptance count of every candidate (what a raw-squeeze
-    // k_xof would still have to do to build the fix-up list), no compaction, one store per block
-#pragma unroll
-    for (int t = 0; t < 14; ++t) {
-      uint32_t d[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int di = 3 * t + e;
-        d[e] = (di & 1) ? s.a[di >> 1].hi : s.a[di >> 1].lo;
-      }
-      int c[8];
-      split12(d[0], d[1], d[2], c);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) cnt += c[e] < Q ? 1 : 0;
-    }
-    chunk_fill(xc<TW>(dst, b), (uint32_t)cnt);
-    if (b == NB - 1) cnt = 256;
-#elif QRK_XOF_TIMING_ONLY == 1
-    // timing probe (tools/build_variant.sh xofperm -DQRK_XOF_TIMING_ONLY=1): the permutations
-    // alone, the state folded into one store per block -- wrong output, never a default build
-    uint32_t f = 0;
-#pragma unroll
-    for (int w = 0; w < 21; ++w) f ^= s.a[w].lo ^ s.a[w].hi;
-    chunk_fill(xc<TW>(dst, b), f);
-    cnt = 256;
-#else
     compact_block<TW>(s, ring_all, rb, cnt, dst, pd);
-#endif
   }
   xof_pend_store<TW>(pd, dst);
-}
-
-// ring entry e (mod 16) of this lane (the default compaction's layout, see compact_block)
-__device__ __forceinline__ uint32_t* ring_entry(char* ring_all, uint32_t rb, int e) {
-  return (uint32_t*)(ring_all + ((uint32_t)(e & 15) << 8 | rb));
 }
 
 // One SampleNTT entry inst = (x K + y) C + hs from scratch: SHAKE128(rho || x || y), ALL = false:
@@ -674,70 +398,32 @@ __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int x
 }
 
 // FIX == false: every entry squeezes exactly 3 blocks (uniform across the wave); the ~0.7 % that
-// still lack 256 values get a fix-up slot (a resume record, or the from-scratch list past the cap).
+// still lack 256 values go on the fix-up list.
 // FIX == true: one lane per slot completes the entry (rewriting identical chunks on the
 // from-scratch path), so the rare 4th block never idles a whole wave.
 template <int K, bool FIX>
-__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
                                              size_t n, size_t C, XUnit* __restrict__ out,
                                              uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix,
                                              uint32_t* __restrict__ fixrec) {
   __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
-#if QRK_XOF_ACC
-  const uint32_t rb = (threadIdx.x >> 7) * 8192 + ((threadIdx.x >> 6) & 1) * 256 + (threadIdx.x & 63) * 4;
-#else
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;
-#endif
   char* ring = (char*)ring_all;
-  const size_t cap = QRK_XOF_RESUME ? xof_rec_cap(K, C) : 0;
   if constexpr (!FIX) {
     const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (inst >= (size_t)K * K * C || inst % C >= n) return;
     KState s;
     xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
     int cnt = 0;
-    xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(out, xwrap(inst)), ring, rb);
-    if (cnt < 256) {
-      const size_t slot = atomicAdd(nfix, 1u);
-      if (slot < cap) {
-        uint32_t* rec = fixrec + slot * XOF_REC_WORDS;
-        rec[0] = (uint32_t)inst;
-        rec[1] = (uint32_t)cnt;
-#pragma unroll
-        for (int i = 0; i < 25; ++i) {
-          rec[2 + 2 * i] = s.a[i].lo;
-          rec[3 + 2 * i] = s.a[i].hi;
-        }
-        const int base = cnt & ~7;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (base + j < cnt) rec[52 + j] = *ring_entry(ring, rb, base + j);
-      } else {
-        fix[slot - cap] = (uint32_t)inst;
-      }
-    }
+    xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(out, inst), ring, rb);
+    if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
   } else {
     const size_t stride = (size_t)gridDim.x * 256, limit = (size_t)*nfix;
 #pragma unroll 1
     for (size_t r = (size_t)blockIdx.x * 256 + threadIdx.x; r < limit; r += stride) {
-      if (r < cap) {
-        const uint32_t* rec = fixrec + r * XOF_REC_WORDS;
-        const size_t inst = rec[0];
-        int cnt = (int)rec[1];
-        KState s;
-#pragma unroll
-        for (int i = 0; i < 25; ++i) s.a[i] = {rec[2 + 2 * i], rec[3 + 2 * i]};
-        const int base = cnt & ~7;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (base + j < cnt) *ring_entry(ring, rb, base + j) = rec[52 + j];
-        XUnit* dst = xent<XTW>(out, inst);
-        xof_blocks<true, MAX_XOF_BLOCKS, XTW>(s, cnt, dst, ring, rb);
-      } else {
-        const size_t inst = fix[r - cap];
-        xof_entry<K, true, XTW>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring,
-                                rb);
-      }
+      const size_t inst = fix[r];
+      xof_entry<K, true, XTW>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring,
+                              rb);
     }
   }
 }
@@ -768,7 +454,7 @@ __device__ __forceinline__ void prf_inst(const uint64_t* __restrict__ seed, int 
 }
 
 template <int ETA1, int ETA2>
-__global__ __launch_bounds__(256) QRK_XOF_ATTR void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
                                              int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
   const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (inst >= (size_t)nprf * C || inst % C >= n) return;
@@ -862,7 +548,7 @@ __device__ __forceinline__ void front_encaps_hs(const uint8_t* __restrict__ pk, 
   }
 }
 template <int K>
-__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_encaps(const uint8_t* __restrict__ pk,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_front_encaps(const uint8_t* __restrict__ pk,
                                                       const uint8_t* __restrict__ coins, size_t n,
                                                       uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
   const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -895,25 +581,8 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
 }
-// The two halves of k_front_decaps as separate launches: J(z || c) needs only the inputs, so on the
-// single-stream schedule it runs on the side stream beside k_xof and the decrypt core
-// (QRK_J_SIDE); G(m' || h) follows the decrypt core on the main stream.
 template <int K>
-__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_j_decaps(const uint8_t* __restrict__ ct,
-                                                  const uint8_t* __restrict__ sk, size_t n, uint64_t* __restrict__ kbar) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
-  j_decaps_hs<K>(ct, sk, hs, kbar);
-}
-template <int K>
-__global__ __launch_bounds__(256) void k_g_decaps(const uint8_t* __restrict__ sk, const uint64_t* __restrict__ mprime,
-                                                  size_t n, uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
-  g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
-}
-template <int K>
-__global__ __launch_bounds__(256) QRK_FRONT_ATTR void k_front_decaps(const uint8_t* __restrict__ ct,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_front_decaps(const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk,
                                                       const uint64_t* __restrict__ mprime, size_t n,
                                                       uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
@@ -938,25 +607,12 @@ constexpr int PBUF = 272;
 // group stride is 368 dwords = 16 (mod 32): the two 16-lane groups that share a ds_* bank
 // half (lanes 0-31 / 32-63) then use disjoint bank sets for every access pattern above.
 constexpr int RAWW = 44;
-// QRK_RAW_ALIAS 1: the byte staging shares the polynomial image's words.  No code path holds a
-// polynomial in the image while it stages bytes: pack_bits / flush_* run after the last
-// transpose of a row and end with a group sync before the next transpose, load_bits ends with one
-// before its caller's first transpose.  1088 B per group instead of 1472 (the encrypt core's
-// SampleNTT prefetch buffer needs the room at 4 waves / SIMD).
-#ifndef QRK_RAW_ALIAS
-#define QRK_RAW_ALIAS 0
-#endif
+// (Aliasing the byte staging onto the polynomial image -- 1088 B per group instead of 1472 -- was
+// only needed by the rejected LDS-DMA matrix prefetch)
 struct GroupLds {
-#if QRK_RAW_ALIAS
-  union {
-    int poly[PBUF];
-    uint64_t raw[RAWW];
-  };
-#else
   int poly[PBUF];
   uint64_t raw[RAWW];
   int pad[8];
-#endif
 };
 static_assert(sizeof(GroupLds) / 4 % 32 == 16, "group stride must be 16 mod 32 dwords");
 constexpr int GROUPS = 16;  // 256 threads
@@ -1170,11 +826,8 @@ __device__ __forceinline__ void ntt_fwd_f(PF16& p, float* buf, int L) {
 // FIPS 203 Alg. 10 in fp32 (including the 128^-1 scaling).  In: contiguous, |f| <= 1665.
 // Out: stride layout, |f| <= 1665.  Gentleman-Sande sums double per layer; the sums of
 // every second layer are reduced, so |y - x| <= 6660 at every twiddle product.  The last
-// layer folds the scaling in (QRK_INV_FOLD): x + y times 128^-1 = -26 and y - x times
+// layer folds the scaling in: x + y times 128^-1 = -26 and y - x times
 // zeta_1 128^-1, instead of a separate product for all 16 outputs.
-#ifndef QRK_INV_FOLD
-#define QRK_INV_FOLD 1
-#endif
 __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
   {
     float z[4];
@@ -1211,7 +864,7 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
   }
   contig_to_stride_f(p, buf, L);
 #pragma unroll
-  for (int lg = 3; lg >= (QRK_INV_FOLD ? 1 : 0); --lg) {
+  for (int lg = 3; lg >= (1 ? 1 : 0); --lg) {
     const int step = 8 >> lg;
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
@@ -1223,7 +876,6 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
       }
     }
   }
-#if QRK_INV_FOLD
   // layer 7 (step 8, zeta_1) with the scaling: |x + y|, |y - x| <= 2 * 6660, far inside the
   // modmul_f bound for the small factors
 #pragma unroll
@@ -1232,10 +884,6 @@ __device__ __forceinline__ void ntt_inv_f(PF16& p, float* buf, int L) {
     p.v[m] = modmul_f(x + y, INV128F, (float)(INV128F / 3329.0));
     p.v[m + 8] = modmul_f(y - x, Z1INV128F, (float)(Z1INV128F / 3329.0));
   }
-#else
-#pragma unroll
-  for (int m = 0; m < 16; ++m) p.v[m] = modmul_f(p.v[m], INV128F, (float)(INV128F / 3329.0));
-#endif
 }
 
 // ---- base-case multiplication (FIPS 203 Alg. 11/12) on packed int16 pairs
@@ -1471,7 +1119,7 @@ __device__ __forceinline__ void flush_cmp(GroupLds& g, const CmpWords<D>& c, uin
 
 // SampleNTT consumer: lane L loads coefficients 16L..16L+15 (chunks 2L, 2L+1)
 // of the producer's compacted output -- contiguous layout, no parsing.
-// The batched producer's 12-bit chunks (QRK_XOF_PACK12), spread back to int16 pairs: a pair is 24
+// The batched producer's 12-bit chunks, spread back to int16 pairs: a pair is 24
 // consecutive bits x, (x & 0xFFF) | (x << 4 & 0x0FFF0000) -- about 3 VALU per pair.
 __device__ __forceinline__ PK8 unpack12(const U3& u, const U3& v) {
   const uint32_t w[6] = {u.x, u.y, u.z, v.x, v.y, v.z};
@@ -1487,15 +1135,10 @@ __device__ __forceinline__ PK8 unpack12(const U3& u, const U3& v) {
 }
 template <int TW = 64, bool P12 = false>
 __device__ __forceinline__ PK8 load_sampled(const void* __restrict__ xs_, size_t inst, int L) {
-  if (TW == XTW) inst = xwrap(inst);
   if constexpr (P12) {
     const XUnit* base = xent<TW>((XUnit*)xs_, inst);
-#if QRK_XOF_PAIR24
     const U6 u = base[L * TW];
     return unpack12(u.h[0], u.h[1]);
-#else
-    return unpack12(base[(2 * L) * TW], base[(2 * L + 1) * TW]);
-#endif
   } else {
     const uint4* base = (const uint4*)xs_ + (inst / TW) * 32 * TW + (inst % TW);
     const uint4 u = base[(2 * L) * TW], v = base[(2 * L + 1) * TW];
@@ -1503,44 +1146,7 @@ __device__ __forceinline__ PK8 load_sampled(const void* __restrict__ xs_, size_t
   }
 }
 // the batched cores' view of the SampleNTT output
-#define LOAD_XOF(TW_, inst) load_sampled<(TW_) == 64 ? XTW : (TW_), (TW_) == 64 && QRK_XOF_PACK12>(xof, (inst), L)
-
-// QRK_ENC_GLDS 1 (needs QRK_XOF_PACK12): the batched encrypt core prefetches the next row's matrix
-// entries (and, for v, t_hat's words) global -> LDS with global_load_lds_dwordx3 into a per-wave
-// buffer (lane l's 12 bytes at base + 12 l, read back by the same lane) instead of into 24 VGPRs,
-// so the core fits 4 waves / SIMD.  The compiler does not order LDS reads after an LDS-DMA, hence
-// the explicit vmcnt(0) before the buffer is read.
-#ifndef QRK_ENC_GLDS
-#define QRK_ENC_GLDS 0
-#endif
-// One lane's 24 contiguous bytes (a chunk pair, or 24 bytes of t_hat) global -> LDS as three
-// DMAs: 16 B into slab 0 (lane l at 16 l: the LDS destination of a DMA of S bytes is the wave base
-// + S l, and a 12-byte DMA also advances 16 B per lane, profiles/r3/glds12_layout_probe.txt), 4 B
-// into slab 1 and 4 B into slab 2 -- 1536 B per wave, no padding.  ab: the entry's 384 dwords.
-__device__ __forceinline__ void glds24(const void* gsrc, uint32_t* ab) {
-  const char* g = (const char*)gsrc;
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)ab, 16, 0, 0);
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 16),
-                                   (__attribute__((address_space(3))) void*)(ab + 256), 4, 0, 0);
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + 20),
-                                   (__attribute__((address_space(3))) void*)(ab + 320), 4, 0, 0);
-}
-__device__ __forceinline__ void glds24_read(const uint32_t* ab, int wl, U3& lo, U3& hi) {
-  const uint4 a = ((const uint4*)ab)[wl];
-  lo = U3{a.x, a.y, a.z};
-  hi = U3{a.w, ab[256 + wl], ab[320 + wl]};
-}
-__device__ __forceinline__ void glds_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// issue row `row`'s K entries (inst = (row K + j) Cx + hxs) into the wave's buffer
-template <int K>
-__device__ __forceinline__ void glds_row(const void* xof, size_t Cx, size_t hxs, int row, int L, uint32_t* ab) {
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const size_t inst = xwrap(((size_t)row * K + j) * Cx + hxs);
-    glds24(xent<XTW>((XUnit*)xof, inst) + L * XTW, ab + 384 * j);
-  }
-}
+#define LOAD_XOF(TW_, inst) load_sampled<(TW_) == 64 ? XTW : (TW_), (TW_) == 64>(xof, (inst), L)
 
 // ByteDecode_12 (reduced mod q) of a 384-byte NTT-domain polynomial into packed
 // pairs; `bad` collects the FIPS 203 section 7.2 modulus-check failure.
@@ -1555,7 +1161,6 @@ __device__ __forceinline__ PK8 decode12_w(uint64_t a, uint64_t b, uint64_t c, bo
   split12((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, v);
   split12((uint32_t)(b >> 32), (uint32_t)c, (uint32_t)(c >> 32), v + 8);
   PK8 r;
-#if QRK_CANON_MASK
   // unsigned min(v, v - q) is v mod q for v < 2q (v - q wraps when v < q); the largest
   // coefficient decides the modulus check (two full-rate ops and one max, no lane masks)
   uint32_t mx = 0;
@@ -1566,13 +1171,6 @@ __device__ __forceinline__ PK8 decode12_w(uint64_t a, uint64_t b, uint64_t c, bo
     v[t] = (int)__builtin_elementwise_min(u, u - (uint32_t)Q);
   }
   bad |= mx >= (uint32_t)Q;
-#else
-#pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    bad |= v[t] >= Q;
-    v[t] = v[t] >= Q ? v[t] - Q : v[t];
-  }
-#endif
 #pragma unroll
   for (int u = 0; u < 8; ++u) r.w[u] = pack16(v[2 * u], v[2 * u + 1]);
   return r;
@@ -1605,13 +1203,12 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
-  size_t fix_cap;        // list capacity K^2 C; 8 spare words follow it (QRK_SPLIT part counters)
-  uint32_t* fixrec;      // SampleNTT resume records (QRK_XOF_RESUME)
-  uint64_t* rho;         // QRK_RHO_COMPACT: every handshake's rho, 32 B apart
+  size_t fix_cap;        // list capacity K^2 C; 8 spare words follow it
+  uint64_t* rho;         // every handshake's rho, 32 B apart (k_rho_copy)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
   return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 4 +
-         xof_rec_cap(K, C) * XOF_REC_WORDS / 2 + 4 * C;
+         4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -1632,20 +1229,15 @@ inline ScratchView carve(void* base, int K, size_t C) {
   v.fix = v.nfix + 2;
   v.fix_cap = (size_t)K * K * C;
   p += ((size_t)K * K * C + 2) / 2 + 4;
-  v.fixrec = (uint32_t*)p;
-  p += xof_rec_cap(K, C) * XOF_REC_WORDS / 2;
   v.rho = p;
   return v;
 }
 
-// QRK_RHO_COMPACT 1: k_xof reads rho from a compact copy (32 B per handshake) instead of the
+// k_xof reads rho from a compact copy (32 B per handshake) instead of the
 // keys themselves.  Its K^2 lanes per handshake sit in K^2 different waves, and each wave's 64
 // rho reads at the key stride (1184 B for ML-KEM-768) touch 64 cache lines: rocprofv3 counts
 // 1.2 GB of reads per 2^20-handshake k_xof launch for 33 MB of rho
 // (profiles/r3/rocprof_mlkem768_b20_r3b.json).  The copy is one 32-B read per handshake.
-#ifndef QRK_RHO_COMPACT
-#define QRK_RHO_COMPACT 1
-#endif
 __global__ __launch_bounds__(256) void k_rho_copy(const uint8_t* __restrict__ base, size_t stride, size_t n,
                                                   uint64_t* __restrict__ out) {
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;  // one thread per word
@@ -1686,7 +1278,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
-  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see QRK_XOF_SUB)
+  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see 0)
   const size_t hs = off + hl;                 // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
   const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
@@ -1761,15 +1353,10 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
                                                       uint8_t* __restrict__ ct, int32_t* __restrict__ status,
                                                       const uint64_t* __restrict__ kprime,
-                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g,
-                                                      uint32_t* ab = nullptr) {
+                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
-  // ab: this wave's LDS prefetch buffer (QRK_ENC_GLDS; the batched kernel only)
-  constexpr bool GL = QRK_ENC_GLDS && QRK_XOF_PACK12 && QRK_XOF_PAIR24 && QRK_ENC_PREFETCH && QRK_EK_PREFETCH && TW == 64;
-  const int wl = threadIdx.x & 63;
-  (void)wl, (void)ab;
   const bool active = hs_raw < n;
-  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see QRK_XOF_SUB)
+  const size_t hl = active ? hs_raw : n - 1;  // index in this launch
   const size_t hs = off + hl;                 // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
   const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
@@ -1777,7 +1364,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
-  if constexpr (GL) glds_row<K>(xof, Cx, hxs, 0, L, ab);  // row 0's entries land during the NTT(y_j)
 
   BOp yb[K];
   {
@@ -1795,54 +1381,24 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   }
   SS_MARK(TW == 16 && L == 0, 5);
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
-  // QRK_ENC_PREFETCH: row i+1's matrix entries and the next CBD words are loaded one row
-  // ahead (latency hidden inside the wave); 0: each entry is loaded as the basemul needs it
-  // (fewer live registers, latency hidden by more resident waves).  Issuing the first row's
-  // entries before the K NTT(y_j) instead was 3 % slower (profiles/r3/ab_core_arith_c.jsonl).
-#if QRK_ENC_PREFETCH
+  // Row i+1's matrix entries and the next CBD words are loaded one row ahead (latency hidden
+  // inside the wave; loading each entry as the basemul needs it, at 4 waves / SIMD, was slower).
+  // Issuing the first row's entries before the K NTT(y_j) instead was 3 % slower
+  // (profiles/r3/ab_core_arith_c.jsonl).
   PK8 an[K];
-  if constexpr (!GL) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * Cx + hxs);
-  }
-#endif
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * Cx + hxs);
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
-  // one u-row; LAST: the final row (QRK_EK_PREFETCH peels it, so its prefetch is t_hat's words)
+  // one u-row; LAST: the final row (peeled, so its prefetch is t_hat's words: the core waited on
+  // memory 25-29 % of its wave time before, profiles/r2/sq_mlkem768_b20_r2b.txt)
   auto row = [&](int i, auto last_t) {
     constexpr bool LAST = decltype(last_t)::value;
     int acc[16];
 #pragma unroll
     for (int t = 0; t < 16; ++t) acc[t] = 0;
-    if constexpr (GL) {
-      glds_wait();
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        U3 lo, hi;
-        glds24_read(ab + 384 * j, wl, lo, hi);
-        basemul_acc(acc, unpack12(lo, hi), yb[j]);
-      }
-    } else {
-#if QRK_ENC_PREFETCH
-#pragma unroll
-      for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
-#else
-#pragma unroll
-      for (int j = 0; j < K; ++j) basemul_acc(acc, LOAD_XOF(TW, (size_t)(i * K + j) * Cx + hxs), yb[j]);
-#endif
-    }
+    for (int j = 0; j < K; ++j) basemul_acc(acc, an[j], yb[j]);
     const CbdRaw ecur = er;
-    if constexpr (GL) {
-      // the buffer's reads have landed in registers (the basemuls used them): refill it
-      if (!LAST && i + 1 < K) {
-        glds_row<K>(xof, Cx, hxs, i + 1, L, ab);
-      } else if (LAST) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          glds24(ek + 384 * j + 24 * L, ab + 384 * j);
-        }
-      }
-    } else {
-#if QRK_ENC_PREFETCH
     if (!LAST) {
       if (i + 1 < K) {
 #pragma unroll
@@ -1857,8 +1413,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
         const uint2 a = e[0], b = e[1], c = e[2];
         an[j].w[0] = a.x, an[j].w[1] = a.y, an[j].w[2] = b.x, an[j].w[3] = b.y, an[j].w[4] = c.x, an[j].w[5] = c.y;
       }
-    }
-#endif
     }
     er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
     PF16 uf;
@@ -1879,14 +1433,9 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     else
       flush_bits<DU>(g, c + 32 * DU * i, nullptr, diff, active, L);
   };
-#if QRK_ENC_PREFETCH && QRK_EK_PREFETCH
 #pragma unroll 1
   for (int i = 0; i < K - 1; ++i) row(i, std::false_type{});
   row(K - 1, std::true_type{});
-#else
-#pragma unroll 1
-  for (int i = 0; i < K; ++i) row(i, std::false_type{});
-#endif
   SS_MARK(TW == 16 && L == 0, 6);
   // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
   {
@@ -1896,23 +1445,12 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     bool bad = false;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-#if QRK_ENC_PREFETCH && QRK_EK_PREFETCH
       uint32_t w[6];
-      if constexpr (GL) {
-        if (j == 0) glds_wait();
-        U3 u, v;
-        glds24_read(ab + 384 * j, wl, u, v);
-        w[0] = u.x, w[1] = u.y, w[2] = u.z, w[3] = v.x, w[4] = v.y, w[5] = v.z;
-      } else {
 #pragma unroll
-        for (int t = 0; t < 6; ++t) w[t] = an[j].w[t];
-      }
+      for (int t = 0; t < 6; ++t) w[t] = an[j].w[t];
       const uint64_t a = ((uint64_t)w[1] << 32) | w[0], b = ((uint64_t)w[3] << 32) | w[2],
                      c = ((uint64_t)w[5] << 32) | w[4];
       basemul_acc(acc, decode12_w(a, b, c, bad), yb[j]);
-#else
-      basemul_acc(acc, decode12(ek + 384 * j, bad, L), yb[j]);
-#endif
     }
     PF16 vf;
 #pragma unroll
@@ -1949,7 +1487,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   SS_MARK(TW == 16 && L == 0, 7);
 }
 template <int K, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? QRK_WPE_CORE : (QRK_ENC_GLDS ? 4 : 3)))) void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? 1 : 3))) void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
                                                       const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
@@ -1959,14 +1497,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? QR
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
-#if QRK_ENC_GLDS
-  __shared__ uint32_t abuf[4 * 384 * K];
-  uint32_t* ab = abuf + (threadIdx.x >> 6) * 384 * K;
-#else
-  uint32_t* ab = nullptr;
-#endif
   encrypt_core_hs<K, MODE>(n, C, Cx, off, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
-                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi], ab);
+                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
 }
 
 // ------------------------------------------------------------ K-PKE.Decrypt core
@@ -1982,41 +1514,21 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
 #pragma unroll
   for (int t = 0; t < 16; ++t) acc[t] = 0;
   bool bad = false;
-#if QRK_CT_PREFETCH
-  // the ciphertext rows are loaded one row ahead (u_0 here, then u_{j+1} or v during row j)
-  RawW<DU> cur = raw_load<DU>(c, L);
-#endif
 #pragma unroll 1
   for (int j = 0; j < K; ++j) {
-#if QRK_DK_PREFETCH
     // s_hat_j's 24 bytes per lane, issued before the NTT that precedes their use
     const uint2* e = (const uint2*)(dk + 384 * j + 24 * L);
     const uint2 da = e[0], db = e[1], dc = e[2];
-#endif
     P16 u;
-#if QRK_CT_PREFETCH
-    RawW<DU> nxt;
-    if (j + 1 < K)
-      nxt = raw_load<DU>(c + 32 * DU * (j + 1), L);
-    else
-      nxt = raw_load<DU, DV>(c + 32 * DU * K, L);
-    load_bits_r<DU>(u, cur, g, L);
-    cur = nxt;
-#else
     load_bits<DU>(u, c + 32 * DU * j, g, L);
-#endif
     PF16 uf;
 #pragma unroll
     for (int t = 0; t < 16; ++t) uf.v[t] = i2f(decompress<DU>(u.v[t]));
     contig_to_stride_f(uf, (float*)g.poly, L);
     ntt_fwd_f<true>(uf, (float*)g.poly, L);
-#if QRK_DK_PREFETCH
     basemul_acc(acc,
                 decode12_w(((uint64_t)da.y << 32) | da.x, ((uint64_t)db.y << 32) | db.x, ((uint64_t)dc.y << 32) | dc.x, bad),
                 make_bop_f(uf, L));
-#else
-    basemul_acc(acc, decode12(dk + 384 * j, bad, L), make_bop_f(uf, L));
-#endif
   }
   PF16 w;
 #pragma unroll
@@ -2024,11 +1536,7 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   ntt_inv_f(w, (float*)g.poly, L);
   stride_to_contig_f(w, (float*)g.poly, L);
   P16 v;
-#if QRK_CT_PREFETCH
-  load_bits_r<DV>(v, cur, g, L);
-#else
   load_bits<DV>(v, c + 32 * DU * K, g, L);
-#endif
   uint32_t bits = 0;
 #pragma unroll
   for (int t = 0; t < 16; ++t) {
@@ -2037,7 +1545,7 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
 }
 template <int K>
-__global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
@@ -2060,10 +1568,7 @@ __global__ __launch_bounds__(256) QRK_CORE_ATTR void k_decrypt_core(size_t n, co
 #define QRK_SMALL_MAX 1024
 #endif
 constexpr int ONE_WAVES = 12;  // Encaps / Decaps: 3 waves per SIMD, the 16-lane cores fit in 170 VGPRs
-#ifndef QRK_KG_WAVES
-#define QRK_KG_WAVES 16  // KeyGen (88 VGPRs): every PRF and SampleNTT item of ML-KEM-768 on its own wave
-#endif
-constexpr int KG_WAVES = QRK_KG_WAVES;
+constexpr int KG_WAVES = 16;
 constexpr int MAX_ONE_WAVES = KG_WAVES > ONE_WAVES ? KG_WAVES : ONE_WAVES;
 
 // ordering between lanes of one wave across phases: a workgroup-scope release / acquire around
@@ -2677,27 +2182,16 @@ inline void join(const Streams& s) {
   qrk_chk(hipStreamWaitEvent(s.main, s.join, 0));
 }
 
-// QRK_J_SIDE 1: Decaps' J(z || c) on the side stream beside k_xof / the decrypt core (see k_j_decaps).
-// Byte-exact (the ML-KEM GPU suite passes on it) but no faster: J stretches over k_xof and doubles
-// the decrypt core it overlaps, the chip being VALU-saturated either way
-// (profiles/r2/ab_j_side.jsonl); off by default.
-#ifndef QRK_J_SIDE
-#define QRK_J_SIDE 0
-#endif
 // fixside: run the fix-up on Streams::side (the single-stream schedule's overlap of the
 // latency-bound fix-up with the next kernels on st); the caller joins with fix_join() before
 // the core reads the sampled matrix
 template <int K>
 void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st,
-                const Streams* fixside = nullptr, int part = -1) {
-  // part >= 0 (QRK_SPLIT): SampleNTT part `part` of a split chunk, C = the part's stride, with its own
-  // matrix region, fix-up list and counter (the counters sit in the 8 spare words after the list)
-  XUnit* out = (XUnit*)(part < 0 ? v.xof : v.xof + (size_t)part * K * K * C * XOF_W);
-  uint32_t* fix = part < 0 ? v.fix : v.fix + (size_t)part * K * K * C;
-  uint32_t* nfix = part < 0 ? v.nfix : v.fix + v.fix_cap + part;
-  qrk_chk(hipMemsetAsync(nfix, 0, 4, st));
+                const Streams* fixside = nullptr) {
+  XUnit* out = (XUnit*)v.xof;
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
-             C, out, fix, nfix, v.fixrec);
+             C, out, v.fix, v.nfix, nullptr);
   hipStream_t fs = st;
   if (fixside) {
     fork_wait(st, fixside->side, fixside->fork);
@@ -2708,7 +2202,7 @@ void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const Scr
   // pass would double it
   const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
   QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C, out,
-             fix, nfix, v.fixrec);
+             v.fix, v.nfix, nullptr);
   if (fixside) qrk_chk(hipEventRecord(fixside->join, fs));
 }
 inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }
@@ -2716,28 +2210,10 @@ inline void fix_join(const Streams* fs) {
   if (fs) qrk_chk(hipStreamWaitEvent(fs->main, fs->join, 0));
 }
 
-// QRK_XOF_SUB S > 0: SampleNTT and the core that consumes it run in sub-chunks of S handshakes
-// (k_xof + fix-up + core per sub-chunk, the front hashes and PRFs over the whole chunk first), so
-// the sampled matrix of one sub-chunk (4.6 KB per ML-KEM-768 handshake) is read back from the
-// Infinity Cache instead of HBM.  0: one SampleNTT pass over the chunk.
-#ifndef QRK_XOF_SUB
-#define QRK_XOF_SUB 0
-#endif
-inline bool xof_sub(size_t n) { return QRK_XOF_SUB > 0 && n > (size_t)QRK_XOF_SUB; }
-
-// Where k_xof reads rho: the compact copy (copied here from the keys unless `copy` is false, i.e.
-// KeyGen's front kernel wrote it), or the keys themselves.
-struct RhoSrc {
-  const uint8_t* base;
-  size_t stride;
-  const uint8_t* at(size_t off) const { return base + off * stride; }
-};
-inline RhoSrc rho_src(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st,
-                      bool copy) {
-  if (!QRK_RHO_COMPACT) return {keys_rho, key_stride};
-  if (copy)
-    QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho);
-  return {(const uint8_t*)v.rho, (size_t)32};
+// k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
+inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st) {
+  QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho);
+  return (const uint8_t*)v.rho;
 }
 
 template <int K>
@@ -2756,26 +2232,10 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   }
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
-             v.seeds, QRK_RHO_COMPACT ? v.rho : nullptr);
-  const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, false);
-  if (xof_sub(n)) {
-    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
-               n, C, 2 * K, 2 * K, v.prf);
-    const size_t Cx = round64((size_t)QRK_XOF_SUB);
-    const Streams* fs = fix_side(s);
-    for (size_t off = 0; off < n; off += Cx) {
-      const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
-      fix_join(fs);
-      QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((m + GROUPS - 1) / GROUPS)), dim3(256), 0,
-                 st, m, C, Cx, off, v.xof, v.prf, pk, sk);
-    }
-    QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
-    return hipGetLastError();
-  }
+             v.seeds, v.rho);
   const Streams* fs = fix_side(s);
   fork(s);
-  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
+  launch_xof<K>((const uint8_t*)v.rho, 32, n, C, v, sd, fs);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
              n, C, 2 * K, 2 * K, v.prf);
   join(s);
@@ -2786,27 +2246,6 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   return hipGetLastError();
 }
 
-// QRK_SPLIT P > 1: at full chunks (single-stream schedule with a side stream) the SampleNTT pass
-// runs as P parts on the side stream while the main stream runs the front hash, the PRFs and then
-// the encrypt core part by part, each part's core waiting only for its own matrix.  k_xof is
-// VALU-bound and the encrypt core waits on memory 28-35 % of its time (SQ), so a core part
-// overlaps the next SampleNTT part instead of running alone.
-#ifndef QRK_SPLIT
-#define QRK_SPLIT 0
-#endif
-// OFF by default.  With device-side forks (hipStreamWaitEvent on the caller's NULL-stream event),
-// on three fresh boxes the back-to-back KeyGen -> Encaps sequence on one context
-// (tests/test_gpu_split.py::test_split_back_to_back, the first GPU process on the box) returned
-// ciphertexts that differ from the serial schedule's in every row while the shared secrets matched:
-// the side stream's SampleNTT parts ran on rho the caller's stream had not yet written.  Since the
-// forks are host-ordered (fork_wait) the same test passed as the first process on two fresh boxes,
-// with the matrix poisoned, plus the whole GPU suite on this variant (profiles/r3/split/) -- but
-// the host wait also takes away the pipelining the split lived on: +0.25 % (4 parts) and +0.0 %
-// (8 parts) against the unsplit schedule on one box, where it gained 2.9-3.6 % before.
-static_assert(QRK_SPLIT >= 0 && QRK_SPLIT <= 8, "QRK_SPLIT parts: one event and one spare fix-up counter each, 8 at most");
-#ifndef QRK_SPLIT_MIN
-#define QRK_SPLIT_MIN 262144
-#endif
 // QRK_DEBUG_POISON (environment, tests / tools only): fill the sampled-matrix region with 0xFF
 // before a batched Encaps / Decaps, so a read of an entry the call has not written shows up as a
 // wrong result instead of reusing the previous call's identical matrix.
@@ -2818,52 +2257,6 @@ template <int K>
 void poison_xof(size_t C, const ScratchView& v, hipStream_t st) {
   if (debug_poison()) qrk_chk(hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st));
 }
-constexpr int SPLIT_P = QRK_SPLIT > 1 ? QRK_SPLIT : 1;  // parts (1 when the split is off)
-template <int K>
-bool split_ok(size_t n, size_t C, const Streams& s) {
-  return QRK_SPLIT > 1 && !s.aux && s.side && s.sfork && s.sub[SPLIT_P - 1] && n >= (size_t)QRK_SPLIT_MIN &&
-         C % (64 * SPLIT_P) == 0;
-}
-// QRK_SPLIT_LAG 1: part 0 runs on the main stream after the PRFs and the side stream's parts
-// 1..P-1 start only then, so they overlap the encrypt cores rather than the (VALU-bound) front
-// hash and PRFs; 0: the side stream starts all parts at once.
-#ifndef QRK_SPLIT_LAG
-#define QRK_SPLIT_LAG 0
-#endif
-// the SampleNTT parts; the caller's core for part q waits on s.sub[q].  Called where part 0 may
-// start: with QRK_SPLIT_LAG after the PRFs on main, else right after the rho copy.
-template <int K>
-void launch_xof_split(const RhoSrc& rs, size_t n, size_t C, const ScratchView& v, const Streams& s) {
-  const size_t Cq = C / SPLIT_P;
-  int q0 = 0;
-  if (QRK_SPLIT_LAG) {
-    launch_xof<K>(rs.at(0), rs.stride, std::min(Cq, n), Cq, v, s.main, nullptr, 0);
-    qrk_chk(hipEventRecord(s.sub[0], s.main));
-    q0 = 1;
-  }
-  fork_wait(s.main, s.side, s.sfork);  // after the rho copy / part 0 / the previous chunk's cores
-  for (int q = q0; q < SPLIT_P; ++q) {
-    const size_t off = (size_t)q * Cq, m = off < n ? std::min(Cq, n - off) : 0;
-    if (m) launch_xof<K>(rs.at(off), rs.stride, m, Cq, v, s.side, nullptr, q);
-    qrk_chk(hipEventRecord(s.sub[q], s.side));
-  }
-}
-template <int K, int MODE>
-void launch_core_split(size_t n, size_t C, const ScratchView& v, const Streams& s, const uint8_t* ek, size_t ek_stride,
-                       const uint8_t* m_base, size_t m_stride, uint8_t* ct, int32_t* status, const uint64_t* kprime,
-                       const uint64_t* kbar, uint8_t* ss) {
-  const size_t Cq = C / SPLIT_P;
-  for (int q = 0; q < SPLIT_P; ++q) {
-    qrk_chk(hipStreamWaitEvent(s.main, s.sub[q], 0));
-    const size_t off = (size_t)q * Cq;
-    if (off >= n) continue;
-    const size_t m = std::min(Cq, n - off);
-    QRK_LAUNCH("k_encrypt_core", s.main, (k_encrypt_core<K, MODE>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
-               dim3(256), 0, s.main, m, C, Cq, off, v.xof + (size_t)q * K * K * Cq * XOF_W, v.prf, ek, ek_stride,
-               m_base, m_stride, ct, status, kprime, kbar, ss);
-  }
-}
-
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2877,38 +2270,8 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const Streams* fs = fix_side(s);
   poison_xof<K>(C, v, st);
-  if (split_ok<K>(n, C, s)) {
-    const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, true);
-    if (!QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
-    QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
-               v.seeds);
-    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-               v.seeds, n, C, 2 * K + 1, K, v.prf);
-    if (QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
-    launch_core_split<K, 0>(n, C, v, s, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, nullptr,
-                            nullptr);
-    return hipGetLastError();
-  }
-  if (xof_sub(n)) {
-    const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, st, true);
-    QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
-               v.seeds);
-    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-               v.seeds, n, C, 2 * K + 1, K, v.prf);
-    const size_t Cx = round64((size_t)QRK_XOF_SUB);
-    for (size_t off = 0; off < n; off += Cx) {
-      const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
-      fix_join(fs);
-      QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
-                 dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status,
-                 nullptr, nullptr, nullptr);
-    }
-    return hipGetLastError();
-  }
   fork(s);
-  const RhoSrc rs = rho_src(pk + 384 * K, (size_t)P<K>::PK, n, v, sd, true);
-  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
+  launch_xof<K>(rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, sd), 32, n, C, v, sd, fs);
   QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
              v.seeds);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
@@ -2934,53 +2297,11 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   const Streams* fs = fix_side(s);
-  const bool jside = QRK_J_SIDE && fs;
   poison_xof<K>(C, v, st);
-  if (jside) {  // J(z || c) on the side stream, after this chunk's predecessors on main (kbar reuse)
-    fork_wait(st, fs->side, fs->fork);
-    QRK_LAUNCH("k_j_decaps", fs->side, k_j_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, fs->side, ct, sk, n, v.kbar);
-  }
-  if (split_ok<K>(n, C, s) && !jside) {
-    const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, st, true);
-    if (!QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
-    QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
-               v.seeds, v.kprime, v.kbar);
-    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-               v.seeds, n, C, 2 * K + 1, K, v.prf);
-    if (QRK_SPLIT_LAG) launch_xof_split<K>(rs, n, C, v, s);
-    launch_core_split<K, 1>(n, C, v, s, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
-                            const_cast<uint8_t*>(ct), (int32_t*)nullptr, v.kprime, v.kbar, ss);
-    return hipGetLastError();
-  }
-  if (xof_sub(n) && !jside) {
-    const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, st, true);
-    QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
-               v.seeds, v.kprime, v.kbar);
-    QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-               v.seeds, n, C, 2 * K + 1, K, v.prf);
-    const size_t Cx = round64((size_t)QRK_XOF_SUB);
-    for (size_t off = 0; off < n; off += Cx) {
-      const size_t m = std::min(Cx, n - off);
-      launch_xof<K>(rs.at(off), rs.stride, m, Cx, v, st, fs);
-      fix_join(fs);
-      QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3((unsigned)((m + GROUPS - 1) / GROUPS)),
-                 dim3(256), 0, st, m, C, Cx, off, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK,
-                 (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct), (int32_t*)nullptr, v.kprime, v.kbar,
-                 ss);
-    }
-    return hipGetLastError();
-  }
   fork(s);
-  const RhoSrc rs = rho_src(sk + 768 * K, (size_t)P<K>::SK, n, v, sd, true);
-  launch_xof<K>(rs.base, rs.stride, n, C, v, sd, fs);
+  launch_xof<K>(rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, sd), 32, n, C, v, sd, fs);
   QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-  if (jside)
-    QRK_LAUNCH("k_g_decaps", st, k_g_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, sk, v.mprime, n, v.seeds,
-               v.kprime);
-  else
-    QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
+  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
                v.seeds, v.kprime, v.kbar);
   QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
              v.seeds, n, C, 2 * K + 1, K, v.prf);
@@ -3000,7 +2321,6 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
 }
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
-int mlkem_split_parts() { return QRK_SPLIT > 1 ? QRK_SPLIT : 0; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }
 
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {

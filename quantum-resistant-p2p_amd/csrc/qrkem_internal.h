@@ -48,17 +48,10 @@ inline void qrk_chk(hipError_t e) {
 // (PyTorch's default), and a library stream made to wait on an event recorded there was observed
 // to run ahead -- the SampleNTT chain read keys the previous call had not finished writing
 // ("forks").  The host wait costs the pipelining of back-to-back calls, nothing else.
-#ifndef QRK_FORK_HOST
-#define QRK_FORK_HOST 1
-#endif
 inline void fork_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
   qrk_chk(hipEventRecord(ev, from));
-#if QRK_FORK_HOST
   (void)to;
   qrk_chk(hipEventSynchronize(ev));
-#else
-  qrk_chk(hipStreamWaitEvent(to, ev, 0));
-#endif
 }
 
 #define QRK_LAUNCH(NAME, ST, ...)                   \
@@ -89,8 +82,6 @@ size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 // ML-KEM batches up to this size run as one launch per operation with no scratch key material
 size_t mlkem_small_max();
-// ML-KEM split SampleNTT / core pipeline parts built in (QRK_SPLIT; 0 = off)
-int mlkem_split_parts();
 // ML-KEM KeyGen batches up to this size run one workgroup per SampleNTT / PRF item (latency)
 size_t mlkem_kg_multi_max();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
@@ -102,11 +93,6 @@ struct Streams {
   hipStream_t main = nullptr;
   hipStream_t aux = nullptr;  // nullptr: single-stream schedule
   hipEvent_t fork = nullptr, join = nullptr;
-  // ML-KEM split pipeline (QRK_SPLIT): the fork from main and one event per SampleNTT part on the
-  // side stream -- created for each chunk and released after its launches, so no event is ever
-  // re-recorded while an earlier wait on it may still be pending
-  hipEvent_t sfork = nullptr;
-  hipEvent_t sub[8] = {};
   // the context's side stream even on the single-stream schedule: ML-KEM runs its SampleNTT
   // fix-up kernel there, beside the front hash (nullptr: fix-up on main)
   hipStream_t side = nullptr;

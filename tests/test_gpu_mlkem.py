@@ -263,9 +263,8 @@ def _sample_ntt_needs_4th_block(rho: bytes, i: int, j: int) -> bool:
 @pytest.mark.parametrize("alg,k", [("ML-KEM-768", 3), ("ML-KEM-512", 2)])
 def test_sample_ntt_fixup_resume_and_overflow(engines, alg, k):
     """Every pk of a 1100-handshake batch carries a rho whose matrix has entries that need a 4th
-    SHAKE128 block, so far more than K^2 C / 16 entries need the fix-up: the first ones resume
-    from their saved sponge state (QRK_XOF_RESUME records), the rest overflow to the
-    from-scratch list.  Encaps is byte-exact vs the oracle for every index."""
+    SHAKE128 block, so every handshake has entries on the SampleNTT fix-up list (far more than the
+    ~0.7 % of random keys).  Encaps is byte-exact vs the oracle for every index."""
     import oracle as orc
     rng = np.random.default_rng(77 + k)
     for _ in range(4000):

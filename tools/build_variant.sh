@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an experimental libqrkem variant with extra -D flags (kernel tuning sweeps):
-#   [CSRC=<other csrc dir>] tools/build_variant.sh <tag> -DQRK_AES_COLS=16 ...
+#   [CSRC=<other csrc dir>] tools/build_variant.sh <tag> -DQRK_SMALL_MAX=512 ...
 # Output: quantum-resistant-p2p_amd/qrkem/variants/libqrkem_<tag>.so (git-ignored; load it
 # with QRKEM_LIBRARY=<path>).  The default build is untouched.
 set -euo pipefail
