@@ -91,10 +91,12 @@ def valu_ops_encdec(alg) -> int:
 FP = {"FrodoKEM-640-SHAKE": (640, 15, 16, 168), "FrodoKEM-976-SHAKE": (976, 16, 24, 136),
       "FrodoKEM-1344-SHAKE": (1344, 16, 32, 136), "FrodoKEM-640-AES": (640, 15, 16, 168),
       "FrodoKEM-976-AES": (976, 16, 24, 136), "FrodoKEM-1344-AES": (1344, 16, 32, 136)}
-# AES Gen(A): FIPS-minimal T-table AES-128 = 10 rounds x 16 table lookups per 16-byte block;
-# one ds_read_b32 wave instruction takes 2 LDS cycles (MI355X_MICROARCH.md LDS table) ->
-# 32 lookups per clock per CU
-AES_LOOKUPS_PER_BLOCK = 160
+# AES Gen(A): T-table AES-128 lookups the kernel performs per 16-byte block -- rounds 3-10 (8 x 16);
+# the plaintext is zero except LE16(i) || LE16(j), so rounds 1-2 fold into per-handshake and
+# per-row precompute (aes.cuh) and are not counted (the FIPS-minimal 160 overstated
+# the rate by 1.25x).  One ds_read_b32 wave instruction takes 2 LDS cycles (MI355X_MICROARCH.md
+# LDS table) -> 32 lookups per clock per CU
+AES_LOOKUPS_PER_BLOCK = 128
 LDS_LOOKUP_PEAK = 256 * 32 * 2.4e9
 MFMA_I8_PEAK = 5.0e15  # dense int8 MFMA ops/s (MI355X_MICROARCH.md: I8 = 2x BF16 per clock, BF16 ~2.5 PF dense)
 
@@ -172,7 +174,16 @@ def mlkem_core_ops(k, eta1, kind):
 
 def kernel_ops_per_hs(alg, name, mode):
     """Algorithmic ops one handshake contributes to kernel `name` in one bench step
-    (encaps+decaps, or decaps only) and the bound they are priced against."""
+    (encaps+decaps, or decaps only) and the bound they are priced against.  A multi-role launch
+    ("k_xof+k_front_encaps", mlkem.hip k_pair) carries the sum of its roles' ops (the SampleNTT
+    fix-up, ~0.7 % of the entries, is not counted)."""
+    if "+" in name:
+        parts = [kernel_ops_per_hs(alg, p, mode) for p in name.split("+")]
+        ops = [o for o, _ in parts if o is not None]
+        bounds = {b for o, b in parts if o is not None}
+        if not ops:
+            return None, None
+        return sum(ops), (bounds.pop() if len(bounds) == 1 else "valu")
     calls = 2 if mode == "encdec" else 1  # kernels shared by Encaps and Decaps run once per op
     if alg in HQ:
         wk = hqc_work(alg)
@@ -205,10 +216,6 @@ def kernel_ops_per_hs(alg, name, mode):
         return ((pk + 1 + 135) // 136 + 1) * PERM_OPS, "valu"
     if name == "k_front_decaps":
         return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
-    if name == "k_j_decaps":  # J(z || c) alone (the side-stream half of k_front_decaps)
-        return ((32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
-    if name == "k_g_decaps":  # G(m' || h)
-        return PERM_OPS, "valu"
     if name == "k_prf":
         return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
     if name == "k_encrypt_core":  # Encaps' Encrypt, and Decaps' re-encryption
@@ -790,7 +797,8 @@ def main():
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
     ap.add_argument("--streams", type=int, default=0,
-                    help="library schedule: 0 auto (serial at full chunks), 1 serial, 2 forked")
+                    help="library schedule (qrk_ctx_set_streams): 0 multi-role launches, 1 serial "
+                         "(one kernel per launch); every kernel runs on the caller's stream either way")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
@@ -798,7 +806,8 @@ def main():
     if args.global_log2_batch is not None and (1 << args.global_log2_batch) < args.gpus:
         raise SystemExit(f"--global-log2-batch {args.global_log2_batch}: fewer handshakes than ranks")
     if os.environ.get("WORLD_SIZE") in (None, "") and args.gpus > 1:
-        return launch_ranks(args.gpus, sys.argv[1:])  # before any HIP call: no exec, a child
+        # before any HIP call: no exec, a child (QRK_BENCH_RANK_SCRIPT: a stub rank script, tests only)
+        return launch_ranks(args.gpus, sys.argv[1:], script=os.environ.get("QRK_BENCH_RANK_SCRIPT") or None)
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
     local = env_int("LOCAL_RANK", 0)
@@ -907,8 +916,8 @@ def main():
     prof_live = eng.profile_read() if not args.no_profile else {}
     eng.profile(False)
     # Kernel-in-isolation pass (serial schedule, one untimed step: qrk_ctx_set_streams(1) runs
-    # every kernel of an operation on the caller's stream, the SampleNTT fix-up included), since
-    # overlapping kernels stretch each other's event spans.
+    # one kernel per launch, the SampleNTT fix-up included), since the multi-role launches of the
+    # timed region time two kernels as one.
     prof = {}
     if not args.no_profile:
         eng.set_streams(1)
@@ -1038,4 +1047,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -126,10 +126,9 @@ int qrk_ctx_staging_residue(qrk_ctx *ctx, uint64_t out[3]);
 /* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
  * scratch stays near 8 GiB); 0 for an unknown algorithm. */
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
-/* 0 (default, auto): independent kernel chains of one operation run forked on
- * a side stream and join the caller's stream when a chunk is below 65536
- * handshakes (latency), serially above (throughput); 2: always forked; 1:
- * always serial (kernel timings in isolation). */
+/* Schedule of one operation's kernels, all on the caller's stream: 0 (default) or 2:
+ * independent kernels share multi-role launches (their workgroups interleaved in one grid);
+ * 1: serial, one kernel per launch (kernel timings in isolation). */
 int qrk_ctx_set_streams(qrk_ctx *ctx, int streams);
 
 /* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */
@@ -141,9 +140,12 @@ int qrk_kem_sizes(const char *alg, size_t out[6]);
  * `status` (nullable, device int32[n]) receives -1 for encapsulation keys that
  * fail the FIPS 203 section 7.2 modulus check, else 0.  `stream` is a
  * hipStream_t (NULL = default stream).  Calls are stream-ordered and
- * asynchronous; re-entrant across contexts.  Calls on one context may use
- * different streams: each call's stream first waits until the previous call on
- * that context is done with the context's scratch. */
+ * asynchronous: every kernel of a call runs on `stream`, and with caller-supplied
+ * coins (or none needed) a call returns to the host before its kernels finish.
+ * With coins == NULL the call returns once the OS coins are uploaded (their pinned
+ * copy is wiped then).  Re-entrant across contexts.  Calls on one context may use
+ * different streams: each call's stream first waits, on the device, until the
+ * previous call on that context is done with the context's scratch. */
 int qrk_kem_keypair_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *pk, uint8_t *sk,
                           const uint8_t *coins, void *stream);
 int qrk_kem_encaps_batch(qrk_ctx *ctx, const char *alg, size_t n, uint8_t *ct, uint8_t *ss,

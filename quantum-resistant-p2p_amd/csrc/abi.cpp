@@ -128,8 +128,6 @@ struct qrk_ctx {
   size_t dstage_bytes = 0;
   uint8_t* hstage = nullptr;  // pinned host staging
   size_t hstage_bytes = 0;
-  hipStream_t aux = nullptr;  // side stream for independent kernel chains
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   uint8_t* hs_scratch = nullptr;  // handshake driver: ephemeral sk / ss of one chunk
   size_t hs_scratch_bytes = 0;
   uint8_t* dio = nullptr;         // host-pointer calls: packed device inputs | outputs
@@ -143,27 +141,28 @@ struct qrk_ctx {
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
   hipStream_t io_stream = nullptr;
-  int streams = 0;            // 0: auto (forked below QRK_FORK_MAX per chunk), 1: serial, 2: forked
+  int streams = 0;            // 0 / 2: auto (multi-role launches), 1: serial (one kernel per launch)
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
   hipStream_t last_stream = nullptr;  // ... on this stream
   bool last_valid = false;
+  hipEvent_t ev_up = nullptr;    // end of the OS-coin upload (run_batch)
   std::mutex mu;
 };
 
 // Calls that use a context's scratch are ordered one after another whatever stream each runs
-// on: the new call's stream waits on the event the previous call recorded at its end.  (A
-// device-pointer call on the caller's stream followed by a host-pointer call on the context's
-// own I/O stream would otherwise let the second overwrite scratch the first is still reading.)
+// on: the new call's stream waits, on the device, on the event the previous call recorded at its
+// end.  (A device-pointer call on the caller's stream followed by a host-pointer call on the
+// context's own I/O stream would otherwise let the second overwrite scratch the first is still
+// reading.)  This is the only cross-stream dependency of the library: every kernel of one call
+// runs on that call's stream, so a device-pointer call never blocks the host.
 static int ctx_order(qrk_ctx* ctx, hipStream_t st) {
   if (!ctx->ev_last) {
     hipError_t e = hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming);
     if (e != hipSuccess) return hip_fail("hipEventCreate(last use)", e);
   }
   if (ctx->last_valid && ctx->last_stream != st) {  // same stream: already in order
-    // host-side wait, as for the launchers' forks (fork_wait in qrkem_internal.h): the previous
-    // stream may be the caller's legacy NULL stream
-    hipError_t e = hipEventSynchronize(ctx->ev_last);
-    if (e != hipSuccess) return hip_fail("hipEventSynchronize(last use)", e);
+    hipError_t e = hipStreamWaitEvent(st, ctx->ev_last, 0);
+    if (e != hipSuccess) return hip_fail("hipStreamWaitEvent(last use)", e);
   }
   return 0;
 }
@@ -232,9 +231,6 @@ static int grow_pinned(uint8_t** p, size_t* have, size_t need) {
   return 0;
 }
 
-#ifndef QRK_FORK_MAX
-#define QRK_FORK_MAX 65536
-#endif
 
 static int os_random(uint8_t* out, size_t n) {
   while (n) {
@@ -304,18 +300,15 @@ struct TimerScope {
   ~TimerScope() { g_timer = prev; }
 };
 
-// Zeroes the pinned host and device staging copies of OS-drawn coins when run_batch returns
-// (these are the KeyGen seeds / Encaps messages, i.e. enough to rebuild the keys):
-// waits for the upload and every kernel that reads them, then wipes both, stream-ordered.
+// Zeroes the device staging copy of OS-drawn coins when run_batch returns (these are
+// the KeyGen seeds / Encaps messages, i.e. enough to rebuild the keys), stream-ordered after the
+// kernels that read it.  The pinned host copy is wiped as soon as its upload has completed.
 struct CoinWipe {
   qrk_ctx* ctx;
   hipStream_t st;
   size_t bytes = 0;
   ~CoinWipe() {
-    if (!bytes) return;
-    (void)hipStreamSynchronize(st);
-    OQS_MEM_cleanse(ctx->hstage, bytes);
-    (void)hipMemsetAsync(ctx->dstage, 0, bytes, st);
+    if (bytes) (void)hipMemsetAsync(ctx->dstage, 0, bytes, st);
   }
 };
 
@@ -335,42 +328,34 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   // coins: NULL -> OS CSPRNG, uploaded to device staging
   const uint8_t* coins = (op == Op::KEYPAIR) ? i1 : (op == Op::ENCAPS ? i2 : nullptr);
   const size_t clen = (op == Op::KEYPAIR) ? a.kp_coins : a.enc_coins;
-  bool synth = false;
   // OS coins are KeyGen seeds / Encaps messages: wipe both staged copies on every exit path
   // (declared after last_use, so the device wipe is queued before the call's end event)
   CoinWipe coin_wipe{ctx, st};
   if (op != Op::DECAPS && coins == nullptr) {
+    // The one host wait of the device-pointer API: the pinned copy of the coins is wiped as soon
+    // as it has reached the device, so the call returns after the upload (which the stream
+    // orders behind its earlier work), not after the kernels.
     const size_t bytes = n * clen;
     if (grow_pinned(&ctx->hstage, &ctx->hstage_bytes, bytes)) return -1;
     if (grow_device(ctx, (void**)&ctx->dstage, &ctx->dstage_bytes, bytes, st)) return -1;
-    ctx_quiesce(ctx);  // pinned staging may still feed an earlier call's copy
+    if (!ctx->ev_up) {
+      hipError_t e = hipEventCreateWithFlags(&ctx->ev_up, hipEventDisableTiming);
+      if (e != hipSuccess) return hip_fail("hipEventCreate(upload)", e);
+    }
     if (os_random(ctx->hstage, bytes)) return -1;
+    coin_wipe.bytes = bytes;
     hipError_t e = hipMemcpyAsync(ctx->dstage, ctx->hstage, bytes, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_up, st);
+    if (e == hipSuccess) e = hipEventSynchronize(ctx->ev_up);
+    OQS_MEM_cleanse(ctx->hstage, bytes);
     if (e != hipSuccess) return hip_fail("hipMemcpyAsync(coins)", e);
     coins = ctx->dstage;
-    synth = true;
-    coin_wipe.bytes = bytes;
-  }
-  if (!ctx->aux) {
-    hipError_t e1 = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
-    hipError_t e2 = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-    hipError_t e3 = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail("cannot create side stream/events");
   }
   Streams S;
   S.main = st;
-  // (the fork also shortens single-shot latency: the SampleNTT chain runs beside front + PRF)
-  // The fork overlaps the SampleNTT chain with the front/PRF chain: it shortens small batches
-  // (single-shot latency) but buys ~1% at full chunks, where every kernel already fills the
-  // chip and the overlap only stretches each kernel's span (profiles/r2/ab_streams*.json).
-  const bool fork = ctx->streams == 2 || (ctx->streams == 0 && chunk < QRK_FORK_MAX);
-  S.aux = fork ? ctx->aux : nullptr;
-  // On the auto schedule the ML-KEM SampleNTT fix-up kernel (about one wave per SIMD, latency-bound)
-  // runs on the side stream beside the front hash and PRFs; streams == 1 is the documented serial
-  // schedule (kernel timings in isolation, qrkem.h): no side-stream fix-up there
-  S.side = ctx->streams != 1 ? ctx->aux : nullptr;
-  S.fork = ctx->ev_fork;
-  S.join = ctx->ev_join;
+  // streams == 1: the documented serial schedule (one kernel per launch: per-kernel timings in
+  // isolation, qrkem.h); otherwise independent kernels of one operation share launches
+  S.serial = ctx->streams == 1;
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
@@ -445,10 +430,6 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     // key material of this chunk (seeds, m', K', Kbar, ...) does not outlive the call
     e = cleanse_records(a, m, ctx->scratch, st);
     if (e != hipSuccess) return hip_fail("hipMemsetAsync(cleanse)", e);
-  }
-  if (synth) {
-    hipError_t e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
   }
   return 0;
 }
@@ -807,9 +788,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   if (ctx->kg_cnt) (void)hipFree(ctx->kg_cnt);
-  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
-  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-  if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+  if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
   if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
   delete ctx;
 }
@@ -843,8 +822,11 @@ int qrk_ctx_staging_residue(qrk_ctx* ctx, uint64_t out[3]) {
     if (!len[b]) continue;
     std::vector<uint8_t> tmp(len[b]);
     hipError_t e = hipMemcpy(tmp.data(), src[b], len[b], hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail("hipMemcpy(staging residue)", e);
     for (uint8_t x : tmp) out[1 + b] += x != 0;
+    // the copy may hold expanded key material (PRF / CBD output, FrodoKEM S, HQC x, y): wipe it
+    // before the heap gets it back
+    OQS_MEM_cleanse(tmp.data(), tmp.size());
+    if (e != hipSuccess) return hip_fail("hipMemcpy(staging residue)", e);
   }
   return 0;
 }

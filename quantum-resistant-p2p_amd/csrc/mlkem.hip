@@ -402,31 +402,36 @@ __device__ __forceinline__ int xof_entry(const uint64_t* __restrict__ rho, int x
 // FIX == true: one lane per slot completes the entry (rewriting identical chunks on the
 // from-scratch path), so the rare 4th block never idles a whole wave.
 template <int K, bool FIX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_xof(const uint8_t* __restrict__ rho_base, size_t rho_stride,
-                                             size_t n, size_t C, XUnit* __restrict__ out,
-                                             uint32_t* __restrict__ fix, uint32_t* __restrict__ nfix,
-                                             uint32_t* __restrict__ fixrec) {
-  __shared__ uint32_t ring_all[4 * 16 * 64];  // per wave: [16 entries][64 lanes]
-  const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;
+struct XofArgs {
+  const uint8_t* rho_base;
+  size_t rho_stride, n, C;
+  XUnit* out;
+  uint32_t *fix, *nfix;
+};
+// block vb of nvb (FIX: the grid-stride walk over the list uses nvb)
+template <int K, bool FIX>
+__device__ __forceinline__ void xof_body(const XofArgs<K, FIX>& a, unsigned vb, unsigned nvb, uint32_t* ring_all) {
+  const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;  // ring_all: [wave][16][64]
   char* ring = (char*)ring_all;
   if constexpr (!FIX) {
-    const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (inst >= (size_t)K * K * C || inst % C >= n) return;
+    const size_t inst = (size_t)vb * 256 + threadIdx.x;
+    if (inst >= (size_t)K * K * a.C || inst % a.C >= a.n) return;
     KState s;
-    xof_init(s, (const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), K);
+    xof_init(s, (const uint64_t*)(a.rho_base + (inst % a.C) * a.rho_stride), (int)(inst / a.C), K);
     int cnt = 0;
-    xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(out, inst), ring, rb);
-    if (cnt < 256) fix[atomicAdd(nfix, 1u)] = (uint32_t)inst;
+    xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(a.out, inst), ring, rb);
+    if (cnt < 256) a.fix[atomicAdd(a.nfix, 1u)] = (uint32_t)inst;
   } else {
-    const size_t stride = (size_t)gridDim.x * 256, limit = (size_t)*nfix;
+    const size_t stride = (size_t)nvb * 256, limit = (size_t)*a.nfix;
 #pragma unroll 1
-    for (size_t r = (size_t)blockIdx.x * 256 + threadIdx.x; r < limit; r += stride) {
-      const size_t inst = fix[r];
-      xof_entry<K, true, XTW>((const uint64_t*)(rho_base + (inst % C) * rho_stride), (int)(inst / C), inst, out, ring,
-                              rb);
+    for (size_t r = (size_t)vb * 256 + threadIdx.x; r < limit; r += stride) {
+      const size_t inst = a.fix[r];
+      xof_entry<K, true, XTW>((const uint64_t*)(a.rho_base + (inst % a.C) * a.rho_stride), (int)(inst / a.C), inst,
+                              a.out, ring, rb);
     }
   }
 }
+constexpr int XOF_LDS = 4 * 16 * 64 * 4;  // the 256-thread block's compaction rings
 
 // PRF producer: SHAKE256(seed || N) -> 64*eta bytes; inst = N * C + hs.
 // eta = (N < eta1_upto) ? ETA1 : ETA2.
@@ -453,13 +458,6 @@ __device__ __forceinline__ void prf_inst(const uint64_t* __restrict__ seed, int 
   }
 }
 
-template <int ETA1, int ETA2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_prf(const uint64_t* __restrict__ seeds, size_t n, size_t C,
-                                             int nprf, int eta1_upto, uint64_t* __restrict__ prf) {
-  const size_t inst = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (inst >= (size_t)nprf * C || inst % C >= n) return;
-  prf_inst<ETA1, ETA2>(seeds + (inst % C) * 4, (int)(inst / C), inst, eta1_upto, prf);
-}
 
 template <int K>
 struct P {
@@ -547,13 +545,6 @@ __device__ __forceinline__ void front_encaps_hs(const uint8_t* __restrict__ pk, 
     seeds[hs * 4 + w] = kword(s, 4 + w);
   }
 }
-template <int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_front_encaps(const uint8_t* __restrict__ pk,
-                                                      const uint8_t* __restrict__ coins, size_t n,
-                                                      uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs < n) front_encaps_hs<K>(pk, coins, hs, ss, seeds);
-}
 
 // Decaps front: (K', r') = G(m' || h), Kbar = J(z || c)
 template <int K>
@@ -580,17 +571,6 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
   absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
-}
-template <int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_front_decaps(const uint8_t* __restrict__ ct,
-                                                      const uint8_t* __restrict__ sk,
-                                                      const uint64_t* __restrict__ mprime, size_t n,
-                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ kprime,
-                                                      uint64_t* __restrict__ kbar) {
-  const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (hs >= n) return;
-  g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
-  j_decaps_hs<K>(ct, sk, hs, kbar);
 }
 
 // ============================================================ 16-lane polynomial groups
@@ -1544,13 +1524,6 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
   }
   if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
 }
-template <int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_decrypt_core(size_t n, const uint8_t* __restrict__ ct,
-                                                      const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime) {
-  __shared__ GroupLds lds[GROUPS];
-  const int gi = threadIdx.x >> 4;
-  decrypt_core_hs<K>(n, ct, sk, mprime, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
-}
 
 // ============================================================ small batches: one launch per operation
 // The reference calls one KeyGen / Encaps / Decaps at a time (key_exchange.py:133, 156, 179):
@@ -2101,8 +2074,14 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   } else {  // SampleNTT entry e = x K + y straight into the scratch
     xof_coop<K>(sl.rho, item - 2 * K, (uint16_t*)scr.xs, sl.pbuf, c);
   }
-  // publish, then count in: the last of the NI workgroups of this handshake finishes it
-  __threadfence();
+  // publish, then count in: the last of the NI workgroups of this handshake finishes it.  With a
+  // host-visible completion flag (n == 1, zero-copy pinned outputs) every workgroup's dk stores are
+  // released at system scope before it counts in, so the host-side ordering does not rest on
+  // agent -> system release transitivity across the XCDs' L2s.
+  if (done)
+    __threadfence_system();
+  else
+    __threadfence();
   __syncthreads();
   if (lane == 0) sl.last = (int)(atomicAdd(&cnt[hs], 1u) == (uint32_t)(NI - 1));
   __syncthreads();
@@ -2163,51 +2142,126 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   }
 }
 
+// ============================================================ multi-role launches
+// Every kernel of a call runs on the caller's stream.  Kernels of one operation that do not depend
+// on each other share one launch instead of running on side streams: a multi-role kernel (k_pair)
+// whose workgroups are interleaved in proportion to the two roles' block counts, so both roles are
+// resident on every CU from the first wave to the last.  That overlaps a latency-bound kernel (the
+// SampleNTT fix-up: ~0.7 % of the entries, 4+ sequential permutations per lane) with a
+// throughput-bound one, and keeps the chip full at mid-size batches, where a lane-per-handshake
+// sponge alone is one wave per SIMD.  A role must not use workgroup barriers (its workgroups may
+// share a launch with another role's) -- the roles below synchronise at most within a wave.
+template <int K, bool FIX>
+struct RXof {  // SampleNTT, lane / matrix entry (FIX: the fix-up list, grid-stride over nb blocks)
+  static constexpr int LDS = XOF_LDS;
+  XofArgs<K, FIX> a;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char* lds) const { xof_body<K, FIX>(a, vb, nb, (uint32_t*)lds); }
+};
+template <int K>
+struct RFrontEnc {  // (K, r) = G(m || H(ek)), lane / handshake
+  static constexpr int LDS = 0;
+  const uint8_t *pk, *coins;
+  size_t n;
+  uint8_t* ss;
+  uint64_t* seeds;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const size_t hs = (size_t)vb * 256 + threadIdx.x;
+    if (hs < n) front_encaps_hs<K>(pk, coins, hs, ss, seeds);
+  }
+};
+template <int K>
+struct RFrontDec {  // (K', r') = G(m' || h), Kbar = J(z || c), lane / handshake
+  static constexpr int LDS = 0;
+  const uint8_t *ct, *sk;
+  const uint64_t* mprime;
+  size_t n;
+  uint64_t *seeds, *kprime, *kbar;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const size_t hs = (size_t)vb * 256 + threadIdx.x;
+    if (hs >= n) return;
+    g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
+    j_decaps_hs<K>(ct, sk, hs, kbar);
+  }
+};
+template <int ETA1, int ETA2>
+struct RPrf {  // PRF_eta(seed, N), lane / (N, handshake)
+  static constexpr int LDS = 0;
+  const uint64_t* seeds;
+  size_t n, C;
+  int nprf, eta1_upto;
+  uint64_t* prf;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const size_t inst = (size_t)vb * 256 + threadIdx.x;
+    if (inst >= (size_t)nprf * C || inst % C >= n) return;
+    prf_inst<ETA1, ETA2>(seeds + (inst % C) * 4, (int)(inst / C), inst, eta1_upto, prf);
+  }
+};
+template <int K>
+struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
+  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds);
+  size_t n;
+  const uint8_t *ct, *sk;
+  uint64_t* mprime;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+    const int gi = threadIdx.x >> 4;
+    decrypt_core_hs<K>(n, ct, sk, mprime, (size_t)vb * GROUPS + gi, threadIdx.x & 15, ((GroupLds*)lds)[gi]);
+  }
+};
+
+// Role B takes workgroup w iff floor((w + 1) nb_B / N) > floor(w nb_B / N), N = nb_A + nb_B: the
+// B workgroups are spread evenly over the grid (block-uniform, one scalar division per workgroup).
+template <class A, class B>
+__global__ __launch_bounds__(256) void k_pair(A a, B b) {
+  constexpr int L = A::LDS > B::LDS ? A::LDS : B::LDS;
+  __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
+  const uint64_t N = (uint64_t)a.nb + b.nb, w = blockIdx.x;
+  const uint32_t tb = (uint32_t)(w * b.nb / N), tb1 = (uint32_t)((w + 1) * b.nb / N);
+  if (tb1 != tb)
+    b.run(tb, lds);
+  else
+    a.run((uint32_t)w - tb, lds);
+}
+template <class R>
+__global__ __launch_bounds__(256) void k_role(R r) {
+  constexpr int L = R::LDS;
+  __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
+  r.run(blockIdx.x, lds);
+}
+
 // ============================================================ host launchers
 
 inline unsigned blocks_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
-// Two-stream schedule per chunk: the SampleNTT chain (k_xof, k_xof_fix) only
-// needs rho, so it runs on the side stream while the main stream does the
-// front hashes and PRFs; the core kernel joins both.  The fork is recorded
-// after the previous chunk's core, so reused scratch is never overwritten early.
-inline void fork(const Streams& s) {
-  if (!s.aux) return;
-  fork_wait(s.main, s.aux, s.fork);
-}
-inline void join(const Streams& s) {
-  if (!s.aux) return;
-  qrk_chk(hipEventRecord(s.join, s.aux));
-  qrk_chk(hipStreamWaitEvent(s.main, s.join, 0));
+// two independent kernels of one operation: one multi-role launch, or (serial schedule) one launch
+// each, A first -- the per-kernel timings in isolation
+template <class A, class B>
+void launch_pair(const char* name, const char* name_a, const char* name_b, const A& a, const B& b, const Streams& s) {
+  hipStream_t st = s.main;
+  if (s.serial || !a.nb || !b.nb) {
+    if (a.nb) QRK_LAUNCH(name_a, st, k_role<A>, dim3(a.nb), dim3(256), 0, st, a);
+    if (b.nb) QRK_LAUNCH(name_b, st, k_role<B>, dim3(b.nb), dim3(256), 0, st, b);
+    return;
+  }
+  QRK_LAUNCH(name, st, (k_pair<A, B>), dim3(a.nb + b.nb), dim3(256), 0, st, a, b);
 }
 
-// fixside: run the fix-up on Streams::side (the single-stream schedule's overlap of the
-// latency-bound fix-up with the next kernels on st); the caller joins with fix_join() before
-// the core reads the sampled matrix
+// SampleNTT roles for a chunk of C handshakes (n used): the main pass and its fix-up.  The fix-up
+// covers fix-up rates up to 1/64 (~0.7 % expected) in a single pass, one lane per listed entry:
+// it is latency-bound (4+ sequential permutations per lane), a second grid-stride pass would double it.
 template <int K>
-void launch_xof(const uint8_t* rho, size_t stride, size_t n, size_t C, const ScratchView& v, hipStream_t st,
-                const Streams* fixside = nullptr) {
-  XUnit* out = (XUnit*)v.xof;
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
-  QRK_LAUNCH("k_xof", st, (k_xof<K, false>), dim3(blocks_for((size_t)K * K * C)), dim3(256), 0, st, rho, stride, n,
-             C, out, v.fix, v.nfix, nullptr);
-  hipStream_t fs = st;
-  if (fixside) {
-    fork_wait(st, fixside->side, fixside->fork);
-    fs = fixside->side;
-  }
-  // one lane per listed entry in a single pass for fix-up rates up to 1/64 (~0.7 % expected):
-  // the fix-up is latency-bound (4+ sequential permutations per lane), a second grid-stride
-  // pass would double it
-  const size_t fix_blocks = std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096);
-  QRK_LAUNCH("k_xof_fix", fs, (k_xof<K, true>), dim3((unsigned)fix_blocks), dim3(256), 0, fs, rho, stride, n, C, out,
-             v.fix, v.nfix, nullptr);
-  if (fixside) qrk_chk(hipEventRecord(fixside->join, fs));
+RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix}, blocks_for((size_t)K * K * C)};
 }
-inline const Streams* fix_side(const Streams& s) { return (!s.aux && s.side) ? &s : nullptr; }
-inline void fix_join(const Streams* fs) {
-  if (fs) qrk_chk(hipStreamWaitEvent(fs->main, fs->join, 0));
+template <int K>
+RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
+          (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
 }
 
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
@@ -2216,6 +2270,19 @@ inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_
   return (const uint8_t*)v.rho;
 }
 
+// QRK_DEBUG_POISON (environment, tests / tools only): fill the sampled-matrix region with 0xFF
+// before a batched Encaps / Decaps, so a read of an entry the call has not written shows up as a
+// wrong result instead of reusing the previous call's identical matrix.
+inline bool debug_poison() {
+  static const bool on = std::getenv("QRK_DEBUG_POISON") != nullptr;
+  return on;
+}
+template <int K>
+void poison_xof(size_t C, const ScratchView& v, hipStream_t st) {
+  if (debug_poison()) qrk_chk(hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st));
+}
+
+// KeyGen: front (rho, sigma) -> {SampleNTT || PRFs} -> fix-up -> t_hat rows -> H(ek)
 template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
@@ -2230,33 +2297,22 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
                pk, sk, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
-  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
+  hipStream_t st = s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds, v.rho);
-  const Streams* fs = fix_side(s);
-  fork(s);
-  launch_xof<K>((const uint8_t*)v.rho, 32, n, C, v, sd, fs);
-  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA1>), dim3(blocks_for(2 * K * C)), dim3(256), 0, st, v.seeds,
-             n, C, 2 * K, 2 * K, v.prf);
-  join(s);
-  fix_join(fs);
+  const uint8_t* rho = (const uint8_t*)v.rho;
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
+  launch_pair("k_xof+k_prf", "k_xof", "k_prf", xof_role<K>(rho, n, C, v),
+              RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)}, s);
+  const auto fx = fix_role<K>(rho, n, C, v);
+  QRK_LAUNCH("k_xof_fix", st, (k_role<RXof<K, true>>), dim3(fx.nb), dim3(256), 0, st, fx);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
              n, C, C, (size_t)0, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
 
-// QRK_DEBUG_POISON (environment, tests / tools only): fill the sampled-matrix region with 0xFF
-// before a batched Encaps / Decaps, so a read of an entry the call has not written shows up as a
-// wrong result instead of reusing the previous call's identical matrix.
-inline bool debug_poison() {
-  static const bool on = std::getenv("QRK_DEBUG_POISON") != nullptr;
-  return on;
-}
-template <int K>
-void poison_xof(size_t C, const ScratchView& v, hipStream_t st) {
-  if (debug_poison()) qrk_chk(hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st));
-}
+// Encaps: rho copy -> {SampleNTT || G(m || H(ek))} -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2267,23 +2323,23 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
                coins, ct, ss, status, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
-  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
-  const Streams* fs = fix_side(s);
+  hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
-  fork(s);
-  launch_xof<K>(rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, sd), 32, n, C, v, sd, fs);
-  QRK_LAUNCH("k_front_encaps", st, k_front_encaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, pk, coins, n, ss,
-             v.seeds);
-  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-             v.seeds, n, C, 2 * K + 1, K, v.prf);
-  join(s);
-  fix_join(fs);
+  const uint8_t* rho = rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, st);
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
+  launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v),
+              RFrontEnc<K>{pk, coins, n, ss, v.seeds, blocks_for(n)}, s);
+  launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix",
+              RPrf<P<K>::ETA1, P<K>::ETA2>{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)},
+              fix_role<K>(rho, n, C, v), s);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256),
              0, st, n, C, C, (size_t)0, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr,
              nullptr, nullptr);
   return hipGetLastError();
 }
 
+// Decaps: rho copy -> {SampleNTT || K-PKE.Decrypt} -> {G(m' || h), J(z || c) || SampleNTT fix-up}
+// -> PRFs -> re-encryption with the constant-time compare and select
 template <int K>
 hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
                        const Streams& s) {
@@ -2294,19 +2350,18 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
                ss, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
-  hipStream_t st = s.main, sd = s.aux ? s.aux : s.main;
+  hipStream_t st = s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
-  const Streams* fs = fix_side(s);
   poison_xof<K>(C, v, st);
-  fork(s);
-  launch_xof<K>(rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, sd), 32, n, C, v, sd, fs);
-  QRK_LAUNCH("k_decrypt_core", st, k_decrypt_core<K>, dim3(gblocks), dim3(256), 0, st, n, ct, sk, v.mprime);
-  QRK_LAUNCH("k_front_decaps", st, k_front_decaps<K>, dim3(blocks_for(n)), dim3(256), 0, st, ct, sk, v.mprime, n,
-               v.seeds, v.kprime, v.kbar);
-  QRK_LAUNCH("k_prf", st, (k_prf<P<K>::ETA1, P<K>::ETA2>), dim3(blocks_for((2 * K + 1) * C)), dim3(256), 0, st,
-             v.seeds, n, C, 2 * K + 1, K, v.prf);
-  join(s);
-  fix_join(fs);
+  const uint8_t* rho = rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, st);
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
+  launch_pair("k_xof+k_decrypt_core", "k_xof", "k_decrypt_core", xof_role<K>(rho, n, C, v),
+              RDecrypt<K>{n, ct, sk, v.mprime, gblocks}, s);
+  launch_pair("k_front_decaps+k_xof_fix", "k_front_decaps", "k_xof_fix",
+              RFrontDec<K>{ct, sk, v.mprime, n, v.seeds, v.kprime, v.kbar, blocks_for(n)}, fix_role<K>(rho, n, C, v),
+              s);
+  const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
+  QRK_LAUNCH("k_prf", st, (k_role<RPrf<P<K>::ETA1, P<K>::ETA2>>), dim3(prf.nb), dim3(256), 0, st, prf);
   QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, C, (size_t)0, v.xof, v.prf,
              sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
              (int32_t*)nullptr, v.kprime, v.kbar, ss);
@@ -2316,8 +2371,10 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
 }  // namespace mlkem
 
 size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
-  // the multi-workgroup KeyGen keeps one MkScr per handshake in the scratch
-  return std::max(mlkem::scratch_words(a.k, mlkem::round64(chunk)) * 8, mlkem::round64(chunk) * sizeof(mlkem::MkScr));
+  // the multi-workgroup KeyGen (n <= QRK_KG_MULTI_MAX) keeps one MkScr (16 KiB) per handshake in
+  // the scratch; every other path needs scratch_words (about 5.1 KB per ML-KEM-768 handshake)
+  const size_t C = mlkem::round64(chunk);
+  return std::max(mlkem::scratch_words(a.k, C) * 8, std::min(C, (size_t)QRK_KG_MULTI_MAX) * sizeof(mlkem::MkScr));
 }
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }

@@ -43,17 +43,6 @@ inline void qrk_chk(hipError_t e) {
   if (e != hipSuccess && g_launch_err == hipSuccess) g_launch_err = e;
 }
 
-// Order stream `to` after everything enqueued on the caller's stream `from` so far.  The host
-// waits for the event instead of hipStreamWaitEvent(to, ev): `from` may be the legacy NULL stream
-// (PyTorch's default), and a library stream made to wait on an event recorded there was observed
-// to run ahead -- the SampleNTT chain read keys the previous call had not finished writing
-// ("forks").  The host wait costs the pipelining of back-to-back calls, nothing else.
-inline void fork_wait(hipStream_t from, hipStream_t to, hipEvent_t ev) {
-  qrk_chk(hipEventRecord(ev, from));
-  (void)to;
-  qrk_chk(hipEventSynchronize(ev));
-}
-
 #define QRK_LAUNCH(NAME, ST, ...)                   \
   do {                                              \
     if (::qrk::g_timer) ::qrk::g_timer->before(NAME, ST); \
@@ -87,15 +76,13 @@ size_t mlkem_kg_multi_max();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 
-// Main stream (the caller's) plus an optional side stream and two events used
-// to fork/join independent kernel chains inside one operation.
+// Launch context of one call: every kernel of the call runs on `main`, the caller's stream (no
+// side streams, no cross-stream events: a call is stream-ordered and never blocks the host).
 struct Streams {
   hipStream_t main = nullptr;
-  hipStream_t aux = nullptr;  // nullptr: single-stream schedule
-  hipEvent_t fork = nullptr, join = nullptr;
-  // the context's side stream even on the single-stream schedule: ML-KEM runs its SampleNTT
-  // fix-up kernel there, beside the front hash (nullptr: fix-up on main)
-  hipStream_t side = nullptr;
+  // serial schedule: one kernel per launch (per-kernel timings in isolation); otherwise
+  // independent kernels of one operation share multi-role launches (ML-KEM, mlkem.hip)
+  bool serial = false;
   // single-shot completion flag (fine-grained host memory, device address): the one-launch ML-KEM
   // kernels store `ticket` there once their outputs are visible to the host
   uint32_t* done = nullptr;

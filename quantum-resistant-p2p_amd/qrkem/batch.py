@@ -191,9 +191,15 @@ class BatchKEM:
         """Handshakes per internal chunk for this algorithm (FrodoKEM caps it by scratch size)."""
         return int(LIB.qrk_ctx_effective_chunk(self._ctx, self.alg.encode()))
 
+    @property
+    def scratch_bytes(self) -> int:
+        """Device scratch the context holds (grown on demand, never shrunk)."""
+        return int(LIB.qrk_ctx_scratch_bytes(self._ctx))
+
     def set_streams(self, streams: int) -> None:
-        """0: auto (fork below 65536 handshakes per chunk, the default); 2: always fork independent
-        kernel chains onto a side stream; 1: always serial."""
+        """0 (default) / 2: independent kernels of one operation share multi-role launches;
+        1: serial, one kernel per launch (per-kernel timings in isolation).  Every kernel runs on
+        the caller's stream either way."""
         self._check(LIB.qrk_ctx_set_streams(self._ctx, streams), "set_streams")
 
     # ------------------------------------------------------------------ kernel timing

@@ -57,6 +57,35 @@ def test_launch_ranks_runs_children_and_relays_rank0(tmp_path, capsys):
     assert d["n_gpus"] == 2 and d["argv"] == ["--gpus", "2", "--steps", "1"]
 
 
+@pytest.mark.parametrize("fail", [True, False])
+def test_bench_module_exit_code_follows_the_ranks(tmp_path, fail):
+    """`python bench.py --gpus 2` (the driver's multi-GPU invocation) exits non-zero when a rank
+    fails, and 0 when rank 0 prints its line (the launcher's code was dropped)."""
+    import subprocess
+    stub = tmp_path / "stub.py"
+    stub.write_text(textwrap.dedent(f'''
+        import json, os, sys
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        r = dist.get_rank()
+        dist.barrier()
+        if r == 0 and not {fail}:
+            print(json.dumps({{"metric": "stub", "value": 1}}))
+        dist.destroy_process_group()
+        sys.exit(3 if {fail} and r == 1 else 0)
+    '''))
+    env = dict(os.environ, QRK_BENCH_RANK_SCRIPT=str(stub))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    if fail:
+        assert p.returncode != 0, p.stdout + p.stderr
+    else:
+        assert p.returncode == 0, p.stdout + p.stderr
+        assert json.loads(p.stdout.strip().splitlines()[-1])["metric"] == "stub"
+
+
 @pytest.mark.parametrize("world,G,block", [(1, 24, 1 << 20), (2, 24, 1 << 20), (8, 24, 1 << 20), (16, 24, 1 << 20),
                                            (8, 22, 1 << 19), (4, 14, 1 << 12), (8, 14, None), (3, 24, None),
                                            (6, 24, None)])

@@ -1,15 +1,14 @@
-"""The auto schedule -- with the split SampleNTT / encrypt-core pipeline when it is built in
-(QRK_SPLIT in csrc/mlkem.hip, off by default) -- against the serial schedule and the
-C oracle.
+"""The auto schedule (independent kernels of one operation in multi-role launches, every kernel
+on the caller's stream) against the serial schedule (one kernel per launch) and the C oracle,
+and the asynchrony of the device-pointer API.
 
-At full chunks (auto stream mode, n >= 2^18, chunk a multiple of 64 * parts) k_xof runs in parts
-on the context's side stream while the main stream runs the front hash, the PRFs and the encrypt
-core part by part.  n = 300000 makes the last part ragged (74976 of 75008).  Every output of the
-split schedule must equal the serial schedule's (qrk_ctx_set_streams(1), no side stream, no split)
-byte for byte over the whole batch -- KeyGen, Encaps, and Decaps with half the ciphertexts tampered
-(the re-encryption compare and implicit rejection) -- and a sample around every part boundary must
-equal the oracle.  Each stage is compared on its own, so a failure names the stage and counts the
-mismatching rows per part.
+Round 3's side-stream schedule produced wrong ciphertexts in every row when KeyGen and Encaps
+ran back to back on one context as the first GPU process of a box (DESIGN.md section 1,
+"Ordering"); the library now has no side streams at all, and these tests pin both properties the
+redesign is for: byte-exact outputs under back-to-back calls with the sampled matrix poisoned
+(QRK_DEBUG_POISON, set for the whole GPU suite in conftest.py) and a device call that returns to
+the host before its kernels finish.  n = 300000 is a ragged batch (not a multiple of 256); every
+stage is compared on its own, so a failure names the stage and counts its mismatching rows.
 """
 import numpy as np
 import pytest
@@ -23,8 +22,9 @@ PARTS = 4
 
 
 def _boundary_idx(n, parts=PARTS):
+    """the ends of the batch and of each quarter (workgroup and tile boundaries fall among them)"""
     cq = ((n + 63) // 64 * 64) // parts
-    idx = [0, 1, n - 1]
+    idx = [0, 1, 63, 64, 255, 256, n - 1]
     for q in range(1, parts):
         idx += [q * cq - 2, q * cq - 1, q * cq, q * cq + 1]
     return np.unique(np.array([i for i in idx if 0 <= i < n]))
@@ -37,9 +37,9 @@ def _rows_per_part(a, b, n=N, parts=PARTS):
 
 
 @pytest.mark.parametrize("alg", ["ML-KEM-768", "ML-KEM-1024"])
-def test_split_back_to_back(alg):
+def test_back_to_back_auto_vs_serial(alg):
     """KeyGen -> Encaps -> tamper -> Decaps on one auto-schedule context with no host
-    synchronisation in between (calls overlap through the streams), then the serial schedule."""
+    synchronisation in between, then the same on the serial schedule."""
     from qrkem.batch import BatchKEM
     eng = BatchKEM(alg, device=0)
     coins = eng.bench_coins(N, 96, seed=400 + len(alg))
@@ -66,12 +66,12 @@ def test_split_back_to_back(alg):
 
 
 @pytest.mark.parametrize("alg", ["ML-KEM-768", "ML-KEM-1024"])
-def test_split_schedule_equals_serial_and_oracle(alg):
+def test_auto_schedule_equals_serial_and_oracle(alg):
     import oracle as orc
     from qrkem.batch import BatchKEM
-    eng = BatchKEM(alg, device=0)  # auto schedule: split at this size
+    eng = BatchKEM(alg, device=0)  # auto schedule: multi-role launches
     ser = BatchKEM(alg, device=0)
-    ser.set_streams(1)  # serial schedule: no side stream, no split
+    ser.set_streams(1)  # serial schedule: one kernel per launch
     coins = eng.bench_coins(N, 96, seed=300 + len(alg))
     kc, ec = coins[:, :64].contiguous(), coins[:, 64:].contiguous()
 
@@ -108,4 +108,40 @@ def test_split_schedule_equals_serial_and_oracle(alg):
     del pk, sk, ct, ss, bad, ss2, pk_s, sk_s, ct_s, ss_s, ss2_s, coins, kc, ec
     eng.close()
     ser.close()
+    torch.cuda.empty_cache()
+
+
+def test_device_encaps_returns_before_its_kernels_finish():
+    """A 2^20-handshake ML-KEM-768 Encaps on device tensors with device coins is stream-ordered
+    and asynchronous (include/qrkem.h): the call returns while its kernels are still running (the
+    stream reports busy right after the call, and the call takes a small fraction of the time to
+    completion), and its outputs equal a synchronous run's."""
+    import time
+    from qrkem.batch import BatchKEM
+    n = 1 << 20
+    eng = BatchKEM("ML-KEM-768", device=0)
+    coins = eng.bench_coins(n, 96, seed=4242)
+    kc, ec = coins[:, :64].contiguous(), coins[:, 64:].contiguous()
+    pk, _ = eng.keypair(coins=kc)
+    ct0, ss0 = eng.encaps(pk, coins=ec)  # grows the scratch (host-synchronous allocation)
+    torch.cuda.synchronize()
+    warm = (torch.empty_like(ct0), torch.empty_like(ss0))  # caching-allocator blocks for the outputs
+    del warm
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    ct, ss = eng.encaps(pk, coins=ec)
+    t1 = time.perf_counter()
+    busy = not stream.query()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    assert busy, "the stream was idle when encaps returned: the call waited for its kernels"
+    assert (t1 - t0) < 0.5 * (t2 - t0), (t1 - t0, t2 - t0)
+    assert torch.equal(ct, ct0) and torch.equal(ss, ss0)
+    # scratch of a 2^20 ML-KEM-768 chunk: the batched layout (~5.0 KB per handshake: the 12-bit
+    # sampled matrix, PRF words, per-handshake records, fix-up list), not 16 KiB per handshake for
+    # the multi-workgroup KeyGen's slots, of which only QRK_KG_MULTI_MAX are used (ADVICE r3)
+    assert 4800 * n <= eng.scratch_bytes <= 5200 * n, eng.scratch_bytes
+    del pk, ct0, ss0, ct, ss, coins, kc, ec
+    eng.close()
     torch.cuda.empty_cache()
