@@ -214,8 +214,12 @@ def kernel_ops_per_hs(alg, name, mode):
         return calls * 3 * k * k * PERM_OPS, "valu"
     if name == "k_front_encaps" and mode == "encdec":
         return ((pk + 1 + 135) // 136 + 1) * PERM_OPS, "valu"
-    if name == "k_front_decaps":
+    if name == "k_front_decaps":  # G(m' || h) + J(z || c) (rounds 1-3: one kernel)
         return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
+    if name == "k_j_decaps":  # J(z || c)
+        return ((32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
+    if name == "k_g_decaps":  # G(m' || h)
+        return PERM_OPS, "valu"
     if name == "k_prf":
         return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
     if name == "k_encrypt_core":  # Encaps' Encrypt, and Decaps' re-encryption
@@ -798,7 +802,8 @@ def main():
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
     ap.add_argument("--streams", type=int, default=0,
                     help="library schedule (qrk_ctx_set_streams): 0 multi-role launches, 1 serial "
-                         "(one kernel per launch); every kernel runs on the caller's stream either way")
+                         "(one kernel per launch), 2 / 3 multi-role + 4- / 8-part ML-KEM pipeline; every "
+                         "kernel runs on the caller's stream in each")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()

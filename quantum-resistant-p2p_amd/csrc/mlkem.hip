@@ -406,7 +406,8 @@ struct XofArgs {
   const uint8_t* rho_base;
   size_t rho_stride, n, C;
   XUnit* out;
-  uint32_t *fix, *nfix;
+  uint32_t *fix, *nfix;  // this pass's fix-up list and its counter
+  size_t off, Cq;        // the handshakes [off, off + Cq) of the chunk (a pipeline part), or 0, C
 };
 // block vb of nvb (FIX: the grid-stride walk over the list uses nvb)
 template <int K, bool FIX>
@@ -414,10 +415,12 @@ __device__ __forceinline__ void xof_body(const XofArgs<K, FIX>& a, unsigned vb, 
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;  // ring_all: [wave][16][64]
   char* ring = (char*)ring_all;
   if constexpr (!FIX) {
-    const size_t inst = (size_t)vb * 256 + threadIdx.x;
-    if (inst >= (size_t)K * K * a.C || inst % a.C >= a.n) return;
+    const size_t e = (size_t)vb * 256 + threadIdx.x, hs = a.off + e % a.Cq;
+    if (e >= (size_t)K * K * a.Cq || hs >= a.n) return;
+    const int xy = (int)(e / a.Cq);
+    const size_t inst = (size_t)xy * a.C + hs;
     KState s;
-    xof_init(s, (const uint64_t*)(a.rho_base + (inst % a.C) * a.rho_stride), (int)(inst / a.C), K);
+    xof_init(s, (const uint64_t*)(a.rho_base + hs * a.rho_stride), xy, K);
     int cnt = 0;
     xof_blocks<false, 3, XTW>(s, cnt, xent<XTW>(a.out, inst), ring, rb);
     if (cnt < 256) a.fix[atomicAdd(a.nfix, 1u)] = (uint32_t)inst;
@@ -1182,12 +1185,12 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 // Scratch carve-up for a chunk of C handshakes
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
-  uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks) and its length
-  size_t fix_cap;        // list capacity K^2 C; 8 spare words follow it
+  uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks), MAX_PARTS counters
+  size_t fix_cap;        // list capacity K^2 C (a pipeline part q uses [q K^2 Cq, (q + 1) K^2 Cq))
   uint64_t* rho;         // every handshake's rho, 32 B apart (k_rho_copy)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 2) / 2 + 4 +
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 16) / 2 + 4 +
          4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
@@ -1206,9 +1209,9 @@ inline ScratchView carve(void* base, int K, size_t C) {
   v.kbar = p;
   p += 4 * C;
   v.nfix = (uint32_t*)p;
-  v.fix = v.nfix + 2;
+  v.fix = v.nfix + 16;
   v.fix_cap = (size_t)K * K * C;
-  p += ((size_t)K * K * C + 2) / 2 + 4;
+  p += ((size_t)K * K * C + 16) / 2 + 4;
   v.rho = p;
   return v;
 }
@@ -2153,14 +2156,14 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
 // share a launch with another role's) -- the roles below synchronise at most within a wave.
 template <int K, bool FIX>
 struct RXof {  // SampleNTT, lane / matrix entry (FIX: the fix-up list, grid-stride over nb blocks)
-  static constexpr int LDS = XOF_LDS;
+  static constexpr int LDS = XOF_LDS, WPE = 1;
   XofArgs<K, FIX> a;
   unsigned nb;
   __device__ __forceinline__ void run(unsigned vb, char* lds) const { xof_body<K, FIX>(a, vb, nb, (uint32_t*)lds); }
 };
 template <int K>
 struct RFrontEnc {  // (K, r) = G(m || H(ek)), lane / handshake
-  static constexpr int LDS = 0;
+  static constexpr int LDS = 0, WPE = 1;
   const uint8_t *pk, *coins;
   size_t n;
   uint8_t* ss;
@@ -2172,23 +2175,33 @@ struct RFrontEnc {  // (K, r) = G(m || H(ek)), lane / handshake
   }
 };
 template <int K>
-struct RFrontDec {  // (K', r') = G(m' || h), Kbar = J(z || c), lane / handshake
-  static constexpr int LDS = 0;
+struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
+  static constexpr int LDS = 0, WPE = 1;
   const uint8_t *ct, *sk;
-  const uint64_t* mprime;
   size_t n;
-  uint64_t *seeds, *kprime, *kbar;
+  uint64_t* kbar;
   unsigned nb;
   __device__ __forceinline__ void run(unsigned vb, char*) const {
     const size_t hs = (size_t)vb * 256 + threadIdx.x;
-    if (hs >= n) return;
-    g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
-    j_decaps_hs<K>(ct, sk, hs, kbar);
+    if (hs < n) j_decaps_hs<K>(ct, sk, hs, kbar);
+  }
+};
+template <int K>
+struct RGDec {  // (K', r') = G(m' || h), lane / handshake
+  static constexpr int LDS = 0, WPE = 1;
+  const uint8_t* sk;
+  const uint64_t* mprime;
+  size_t n;
+  uint64_t *seeds, *kprime;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const size_t hs = (size_t)vb * 256 + threadIdx.x;
+    if (hs < n) g_decaps_hs<K>(sk, mprime, hs, seeds, kprime);
   }
 };
 template <int ETA1, int ETA2>
 struct RPrf {  // PRF_eta(seed, N), lane / (N, handshake)
-  static constexpr int LDS = 0;
+  static constexpr int LDS = 0, WPE = 1;
   const uint64_t* seeds;
   size_t n, C;
   int nprf, eta1_upto;
@@ -2202,7 +2215,7 @@ struct RPrf {  // PRF_eta(seed, N), lane / (N, handshake)
 };
 template <int K>
 struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
-  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds);
+  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = 1;
   size_t n;
   const uint8_t *ct, *sk;
   uint64_t* mprime;
@@ -2213,10 +2226,33 @@ struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
   }
 };
 
+template <int K, int MODE>
+struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and select), 16 lanes / hs,
+                // over the handshakes [off, off + m) of the chunk; xof points at entry `off`
+  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = K == 4 ? 1 : 3;
+  size_t m, C, off;
+  const uint64_t *xof, *prf;
+  const uint8_t* ek;
+  size_t ek_stride;
+  const uint8_t* m_base;
+  size_t m_stride;
+  uint8_t* ct;
+  int32_t* status;
+  const uint64_t *kprime, *kbar;
+  uint8_t* ss;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+    const int gi = threadIdx.x >> 4;
+    encrypt_core_hs<K, MODE>(m, C, C, off, xof, prf, ek, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
+                             (size_t)vb * GROUPS + gi, threadIdx.x & 15, ((GroupLds*)lds)[gi]);
+  }
+};
+
 // Role B takes workgroup w iff floor((w + 1) nb_B / N) > floor(w nb_B / N), N = nb_A + nb_B: the
 // B workgroups are spread evenly over the grid (block-uniform, one scalar division per workgroup).
 template <class A, class B>
-__global__ __launch_bounds__(256) void k_pair(A a, B b) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(A::WPE > B::WPE ? A::WPE : B::WPE))) void k_pair(
+    A a, B b) {
   constexpr int L = A::LDS > B::LDS ? A::LDS : B::LDS;
   __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
   const uint64_t N = (uint64_t)a.nb + b.nb, w = blockIdx.x;
@@ -2226,8 +2262,29 @@ __global__ __launch_bounds__(256) void k_pair(A a, B b) {
   else
     a.run((uint32_t)w - tb, lds);
 }
+// Three roles: C's workgroups are spread over the grid the same way, A and B share the rest.
+template <class A, class B, class C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    A::WPE > B::WPE ? (A::WPE > C::WPE ? A::WPE : C::WPE) : (B::WPE > C::WPE ? B::WPE : C::WPE)))) void k_tri(A a, B b,
+                                                                                                            C c) {
+  constexpr int L1 = A::LDS > B::LDS ? A::LDS : B::LDS;
+  constexpr int L = L1 > C::LDS ? L1 : C::LDS;
+  __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
+  const uint64_t N = (uint64_t)a.nb + b.nb + c.nb, w = blockIdx.x;
+  const uint32_t tc = (uint32_t)(w * c.nb / N), tc1 = (uint32_t)((w + 1) * c.nb / N);
+  if (tc1 != tc) {
+    c.run(tc, lds);
+    return;
+  }
+  const uint64_t N2 = (uint64_t)a.nb + b.nb, w2 = w - tc;
+  const uint32_t tb = (uint32_t)(w2 * b.nb / N2), tb1 = (uint32_t)((w2 + 1) * b.nb / N2);
+  if (tb1 != tb)
+    b.run(tb, lds);
+  else
+    a.run((uint32_t)w2 - tb, lds);
+}
 template <class R>
-__global__ __launch_bounds__(256) void k_role(R r) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R::WPE))) void k_role(R r) {
   constexpr int L = R::LDS;
   __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
   r.run(blockIdx.x, lds);
@@ -2250,18 +2307,55 @@ void launch_pair(const char* name, const char* name_a, const char* name_b, const
   }
   QRK_LAUNCH(name, st, (k_pair<A, B>), dim3(a.nb + b.nb), dim3(256), 0, st, a, b);
 }
+template <class A, class B, class C>
+void launch_tri(const char* name, const char* name_a, const char* name_b, const char* name_c, const A& a, const B& b,
+                const C& c, const Streams& s) {
+  hipStream_t st = s.main;
+  if (s.serial) {
+    QRK_LAUNCH(name_a, st, k_role<A>, dim3(a.nb), dim3(256), 0, st, a);
+    QRK_LAUNCH(name_b, st, k_role<B>, dim3(b.nb), dim3(256), 0, st, b);
+    QRK_LAUNCH(name_c, st, k_role<C>, dim3(c.nb), dim3(256), 0, st, c);
+    return;
+  }
+  QRK_LAUNCH(name, st, (k_tri<A, B, C>), dim3(a.nb + b.nb + c.nb), dim3(256), 0, st, a, b, c);
+}
 
 // SampleNTT roles for a chunk of C handshakes (n used): the main pass and its fix-up.  The fix-up
 // covers fix-up rates up to 1/64 (~0.7 % expected) in a single pass, one lane per listed entry:
 // it is latency-bound (4+ sequential permutations per lane), a second grid-stride pass would double it.
+// Part q of P (Cq = C / P handshakes, q = 0 / P = 1: the whole chunk) has its own fix-up list and
+// counter, so a part's fix-up can run while the next part's SampleNTT is still filling its list.
 template <int K>
-RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix}, blocks_for((size_t)K * K * C)};
+RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, int q = 0, int P = 1) {
+  const size_t Cq = C / P;
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix + (size_t)q * K * K * Cq, v.nfix + q, (size_t)q * Cq, Cq},
+          blocks_for((size_t)K * K * Cq)};
 }
 template <int K>
-RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
-          (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
+RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, int q = 0, int P = 1) {
+  const size_t Cq = C / P;
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix + (size_t)q * K * K * Cq, v.nfix + q, (size_t)q * Cq, Cq},
+          (unsigned)std::min<size_t>((size_t)K * K * Cq / (64 * 256) + 1, 4096)};
+}
+// the K-PKE.Encrypt role over part q (MODE 0: Encaps, ek = pk, m = coins; MODE 1: the Decaps
+// re-encryption, ek inside dk, m = m'); nb = 0 for a part past the end of the batch
+template <int K, int MODE>
+RCore<K, MODE> core_role(size_t n, size_t C, const ScratchView& v, const uint8_t* ek, size_t ek_stride,
+                         const uint8_t* m_base, size_t m_stride, uint8_t* ct, int32_t* status, uint8_t* ss, int q = 0,
+                         int P = 1) {
+  const size_t Cq = C / P, off = (size_t)q * Cq, m = off < n ? std::min(Cq, n - off) : 0;
+  return {m, C, off, v.xof + off * XOF_W, v.prf, ek, ek_stride, m_base, m_stride, ct, status, v.kprime, v.kbar, ss,
+          (unsigned)((m + GROUPS - 1) / GROUPS)};
+}
+template <class R>
+void launch_one(const char* name, const R& r, const Streams& s) {
+  if (r.nb) QRK_LAUNCH(name, s.main, k_role<R>, dim3(r.nb), dim3(256), 0, s.main, r);
+}
+// pipeline parts for a chunk of C handshakes: 0 (no pipeline) unless the schedule asks for one
+// and the parts are whole tiles of the 64-entry layouts
+inline int pipeline_parts(const Streams& s, size_t n, size_t C) {
+  const int P = s.serial ? 1 : s.parts;
+  return (P >= 4 && P <= 16 && C % (64 * (size_t)P) == 0 && n > (size_t)64 * P) ? P : 1;
 }
 
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
@@ -2312,7 +2406,10 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   return hipGetLastError();
 }
 
-// Encaps: rho copy -> {SampleNTT || G(m || H(ek))} -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt
+// Encaps: rho copy -> {SampleNTT || G(m || H(ek))} -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt.
+// Pipelined (P parts, qrk_ctx_set_streams 2 / 3): launch t runs SampleNTT of part t, the fix-up
+// of part t - 1 and the encrypt core of part t - 2 (plus the front at t = 0, the PRFs at t = 1),
+// so every encrypt-core part but the last shares the chip with VALU-bound Keccak work.
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2326,20 +2423,35 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, st);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
-  launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v),
-              RFrontEnc<K>{pk, coins, n, ss, v.seeds, blocks_for(n)}, s);
-  launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix",
-              RPrf<P<K>::ETA1, P<K>::ETA2>{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)},
-              fix_role<K>(rho, n, C, v), s);
-  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 0>), dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256),
-             0, st, n, C, C, (size_t)0, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr,
-             nullptr, nullptr);
+  const int NP = pipeline_parts(s, n, C);
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4 * NP, st));
+  const RFrontEnc<K> front{pk, coins, n, ss, v.seeds, blocks_for(n)};
+  const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
+  auto core = [&](int q) {
+    return core_role<K, 0>(n, C, v, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, q, NP);
+  };
+  if (NP == 1) {
+    launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v), front, s);
+    launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix", prf, fix_role<K>(rho, n, C, v), s);
+    launch_one("k_encrypt_core", core(0), s);
+    return hipGetLastError();
+  }
+  launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v, 0, NP), front, s);
+  launch_tri("k_xof+k_prf+k_xof_fix", "k_xof", "k_prf", "k_xof_fix", xof_role<K>(rho, n, C, v, 1, NP), prf,
+             fix_role<K>(rho, n, C, v, 0, NP), s);
+  for (int t = 2; t < NP; ++t)
+    launch_tri("k_xof+k_xof_fix+k_encrypt_core", "k_xof", "k_xof_fix", "k_encrypt_core",
+               xof_role<K>(rho, n, C, v, t, NP), fix_role<K>(rho, n, C, v, t - 1, NP), core(t - 2), s);
+  launch_pair("k_xof_fix+k_encrypt_core", "k_xof_fix", "k_encrypt_core", fix_role<K>(rho, n, C, v, NP - 1, NP),
+              core(NP - 2), s);
+  launch_one("k_encrypt_core", core(NP - 1), s);
   return hipGetLastError();
 }
 
-// Decaps: rho copy -> {SampleNTT || K-PKE.Decrypt} -> {G(m' || h), J(z || c) || SampleNTT fix-up}
-// -> PRFs -> re-encryption with the constant-time compare and select
+// Decaps: rho copy -> {SampleNTT || K-PKE.Decrypt || J(z || c)} -> {G(m' || h) || SampleNTT fix-up}
+// -> PRFs -> re-encryption with the constant-time compare and select.  Pipelined (P parts): launch t
+// runs SampleNTT of part t, the fix-up of part t - 1 and the re-encryption of part t - 3 (plus the
+// decrypt core and J at t = 0, G at t = 1, the PRFs at t = 2).
 template <int K>
 hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
                        const Streams& s) {
@@ -2354,17 +2466,37 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, st);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
-  launch_pair("k_xof+k_decrypt_core", "k_xof", "k_decrypt_core", xof_role<K>(rho, n, C, v),
-              RDecrypt<K>{n, ct, sk, v.mprime, gblocks}, s);
-  launch_pair("k_front_decaps+k_xof_fix", "k_front_decaps", "k_xof_fix",
-              RFrontDec<K>{ct, sk, v.mprime, n, v.seeds, v.kprime, v.kbar, blocks_for(n)}, fix_role<K>(rho, n, C, v),
-              s);
+  const int NP = pipeline_parts(s, n, C);
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4 * NP, st));
+  const RDecrypt<K> dec{n, ct, sk, v.mprime, gblocks};
+  const RJDec<K> jd{ct, sk, n, v.kbar, blocks_for(n)};
+  const RGDec<K> gd{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
-  QRK_LAUNCH("k_prf", st, (k_role<RPrf<P<K>::ETA1, P<K>::ETA2>>), dim3(prf.nb), dim3(256), 0, st, prf);
-  QRK_LAUNCH("k_encrypt_core", st, (k_encrypt_core<K, 1>), dim3(gblocks), dim3(256), 0, st, n, C, C, (size_t)0, v.xof, v.prf,
-             sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32, const_cast<uint8_t*>(ct),
-             (int32_t*)nullptr, v.kprime, v.kbar, ss);
+  auto core = [&](int q) {
+    return core_role<K, 1>(n, C, v, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
+                           const_cast<uint8_t*>(ct), nullptr, ss, q, NP);
+  };
+  if (NP == 1) {
+    launch_tri("k_xof+k_decrypt_core+k_j_decaps", "k_xof", "k_decrypt_core", "k_j_decaps", xof_role<K>(rho, n, C, v),
+               dec, jd, s);
+    launch_pair("k_g_decaps+k_xof_fix", "k_g_decaps", "k_xof_fix", gd, fix_role<K>(rho, n, C, v), s);
+    launch_one("k_prf", prf, s);
+    launch_one("k_encrypt_core", core(0), s);
+    return hipGetLastError();
+  }
+  launch_tri("k_xof+k_decrypt_core+k_j_decaps", "k_xof", "k_decrypt_core", "k_j_decaps",
+             xof_role<K>(rho, n, C, v, 0, NP), dec, jd, s);
+  launch_tri("k_xof+k_g_decaps+k_xof_fix", "k_xof", "k_g_decaps", "k_xof_fix", xof_role<K>(rho, n, C, v, 1, NP), gd,
+             fix_role<K>(rho, n, C, v, 0, NP), s);
+  launch_tri("k_xof+k_prf+k_xof_fix", "k_xof", "k_prf", "k_xof_fix", xof_role<K>(rho, n, C, v, 2, NP), prf,
+             fix_role<K>(rho, n, C, v, 1, NP), s);
+  for (int t = 3; t < NP; ++t)
+    launch_tri("k_xof+k_xof_fix+k_encrypt_core", "k_xof", "k_xof_fix", "k_encrypt_core",
+               xof_role<K>(rho, n, C, v, t, NP), fix_role<K>(rho, n, C, v, t - 1, NP), core(t - 3), s);
+  launch_pair("k_xof_fix+k_encrypt_core", "k_xof_fix", "k_encrypt_core", fix_role<K>(rho, n, C, v, NP - 1, NP),
+              core(NP - 3), s);
+  launch_one("k_encrypt_core", core(NP - 2), s);
+  launch_one("k_encrypt_core", core(NP - 1), s);
   return hipGetLastError();
 }
 

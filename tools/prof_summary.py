@@ -19,7 +19,37 @@ from collections import defaultdict
 from pathlib import Path
 
 
+# ML-KEM multi-role launches (mlkem.hip k_pair / k_tri / k_role): the rocprof name carries the role
+# types; the library's own launch names (QRK_LAUNCH, bench.py's kernel tables) join the roles with '+'
+ROLES = {"RXof<{k}, false>": "k_xof", "RXof<{k}, true>": "k_xof_fix", "RFrontEnc": "k_front_encaps", "RPrf": "k_prf",
+         "RDecrypt": "k_decrypt_core", "RJDec": "k_j_decaps", "RGDec": "k_g_decaps"}
+
+
+def role_name(t: str) -> str:
+    t = t.strip().replace("qrk::mlkem::", "")
+    m = re.match(r"RXof<\d+, (true|false)>", t)
+    if m:
+        return "k_xof_fix" if m.group(1) == "true" else "k_xof"
+    for k, v in ROLES.items():
+        if t.startswith(k):
+            return v
+    return t
+
+
 def short(name: str) -> str:
+    m = re.search(r"(k_pair|k_tri|k_role)<(.*)>\(", name)
+    if m:
+        args, depth, cur = [], 0, ""
+        for ch in m.group(2):
+            if ch == "," and depth == 0:
+                args.append(cur)
+                cur = ""
+                continue
+            depth += ch == "<"
+            depth -= ch == ">"
+            cur += ch
+        args.append(cur)
+        return "+".join(role_name(a) for a in args)
     m = re.search(r"(k_\w+)(<[^(]*>)?\(", name)
     if not m:
         return name.split("(")[0][:60]

@@ -6,6 +6,9 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from prof_summary import short  # noqa: E402  (multi-role launch names)
+
 d = Path(sys.argv[1])
 acc = defaultdict(lambda: defaultdict(float))
 cnt = defaultdict(lambda: defaultdict(int))
@@ -14,10 +17,9 @@ for sub in ("a", "b"):
     if not p.exists():
         continue
     for row in csv.DictReader(open(p)):
-        m = re.search(r"(k_\w+)(<[^(]*>)?\(", row["Kernel_Name"])
-        if not m:
+        if not re.search(r"k_\w+", row["Kernel_Name"]):
             continue
-        k = m.group(1) + (m.group(2) or "")
+        k = short(row["Kernel_Name"])
         acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
         cnt[k][row["Counter_Name"]] += 1
 for k, c in acc.items():

@@ -24,15 +24,15 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from prof_summary import short  # noqa: E402  (multi-role launch names)
+
 PEAK = 78.6432  # T lane-ops/s
 FULL_RATE = 61.26  # v_xor_b32 measured, T lane-ops/s
 
 
 def bench_name(pmc_name: str) -> str:
-    base = pmc_name.split("<")[0]
-    if base == "k_xof" and "true" in pmc_name:
-        return "k_xof_fix"
-    return base
+    return pmc_name.split("<")[0]  # short() already maps the multi-role launches to launch names
 
 
 def main() -> None:
@@ -46,10 +46,9 @@ def main() -> None:
         if not p.exists():
             continue
         for row in csv.DictReader(open(p)):
-            m = re.search(r"(k_\w+)(<[^(]*>)?\(", row["Kernel_Name"])
-            if not m:
+            if not re.search(r"k_\w+", row["Kernel_Name"]):
                 continue
-            k = m.group(1) + (m.group(2) or "")
+            k = short(row["Kernel_Name"])
             acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
             cnt[k][row["Counter_Name"]] += 1
     res = {}
