@@ -800,10 +800,9 @@ def main():
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--mode", choices=["encdec", "decaps-tampered", "handshake", "wire"], default="encdec")
     ap.add_argument("--symmetric", default="AES-256-GCM", help="handshake mode: HKDF key size / info suffix")
-    ap.add_argument("--streams", type=int, default=0,
+    ap.add_argument("--streams", type=int, default=0, choices=[0, 1],
                     help="library schedule (qrk_ctx_set_streams): 0 multi-role launches, 1 serial "
-                         "(one kernel per launch), 2 / 3 multi-role + 4- / 8-part ML-KEM pipeline; every "
-                         "kernel runs on the caller's stream in each")
+                         "(one kernel per launch); every kernel runs on the caller's stream in both")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()

@@ -128,9 +128,7 @@ int qrk_ctx_staging_residue(qrk_ctx *ctx, uint64_t out[3]);
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
 /* Schedule of one operation's kernels, all on the caller's stream: 0 (default): independent
  * kernels share multi-role launches (their workgroups interleaved in one grid); 1: serial, one
- * kernel per launch (kernel timings in isolation); 2 / 3: as 0, and batched ML-KEM Encaps /
- * Decaps additionally run SampleNTT and the encrypt core as a software pipeline over 4 / 8
- * parts of each chunk. */
+ * kernel per launch (kernel timings in isolation).  Any other value: QRK_EINVAL. */
 int qrk_ctx_set_streams(qrk_ctx *ctx, int streams);
 
 /* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */

@@ -141,7 +141,7 @@ struct qrk_ctx {
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
   hipStream_t io_stream = nullptr;
-  int streams = 0;            // 0: multi-role launches, 1: serial, 2 / 3: pipelined in 4 / 8 parts
+  int streams = 0;            // 0: multi-role launches, 1: serial (one kernel per launch)
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
   hipStream_t last_stream = nullptr;  // ... on this stream
   bool last_valid = false;
@@ -356,7 +356,6 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   // streams == 1: the documented serial schedule (one kernel per launch: per-kernel timings in
   // isolation, qrkem.h); otherwise independent kernels of one operation share launches
   S.serial = ctx->streams == 1;
-  S.parts = ctx->streams == 2 ? 4 : ctx->streams == 3 ? 8 : 1;
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
@@ -795,7 +794,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
 }
 
 int qrk_ctx_set_streams(qrk_ctx* ctx, int streams) {
-  if (!ctx || streams < 0 || streams > 3) return fail("streams must be 0 (auto), 1 (serial), 2 or 3 (pipelined)");
+  if (!ctx || streams < 0 || streams > 1) return fail("streams must be 0 (auto) or 1 (serial)");
   std::lock_guard<std::mutex> lk(ctx->mu);
   ctx->streams = streams;
   return 0;

@@ -406,8 +406,7 @@ struct XofArgs {
   const uint8_t* rho_base;
   size_t rho_stride, n, C;
   XUnit* out;
-  uint32_t *fix, *nfix;  // this pass's fix-up list and its counter
-  size_t off, Cq;        // the handshakes [off, off + Cq) of the chunk (a pipeline part), or 0, C
+  uint32_t *fix, *nfix;  // the fix-up list and its counter
 };
 // block vb of nvb (FIX: the grid-stride walk over the list uses nvb)
 template <int K, bool FIX>
@@ -415,9 +414,9 @@ __device__ __forceinline__ void xof_body(const XofArgs<K, FIX>& a, unsigned vb, 
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;  // ring_all: [wave][16][64]
   char* ring = (char*)ring_all;
   if constexpr (!FIX) {
-    const size_t e = (size_t)vb * 256 + threadIdx.x, hs = a.off + e % a.Cq;
-    if (e >= (size_t)K * K * a.Cq || hs >= a.n) return;
-    const int xy = (int)(e / a.Cq);
+    const size_t e = (size_t)vb * 256 + threadIdx.x, hs = e % a.C;
+    if (e >= (size_t)K * K * a.C || hs >= a.n) return;
+    const int xy = (int)(e / a.C);
     const size_t inst = (size_t)xy * a.C + hs;
     KState s;
     xof_init(s, (const uint64_t*)(a.rho_base + hs * a.rho_stride), xy, K);
@@ -1185,8 +1184,7 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 // Scratch carve-up for a chunk of C handshakes
 struct ScratchView {
   uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
-  uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks), MAX_PARTS counters
-  size_t fix_cap;        // list capacity K^2 C (a pipeline part q uses [q K^2 Cq, (q + 1) K^2 Cq))
+  uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks, capacity K^2 C), its counter
   uint64_t* rho;         // every handshake's rho, 32 B apart (k_rho_copy)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
@@ -1210,7 +1208,6 @@ inline ScratchView carve(void* base, int K, size_t C) {
   p += 4 * C;
   v.nfix = (uint32_t*)p;
   v.fix = v.nfix + 16;
-  v.fix_cap = (size_t)K * K * C;
   p += ((size_t)K * K * C + 16) / 2 + 4;
   v.rho = p;
   return v;
@@ -1257,14 +1254,13 @@ __device__ unsigned long long g_ss_trace[32];
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
 template <int K, int TW = 64>
-__device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, size_t off, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
-  const size_t hl = active ? hs_raw : n - 1;  // index in this launch (a SampleNTT sub-chunk, see 0)
-  const size_t hs = off + hl;                 // index in the chunk
+  const size_t hs = active ? hs_raw : n - 1;  // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
-  const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
+  const size_t hxs = hss;                // SampleNTT instance (stride C)
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   BOp sb[K];
@@ -1288,7 +1284,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K) * Cx + hxs);
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K) * C + hxs);
   CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
@@ -1300,7 +1296,7 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K + i + 1) * Cx + hxs);
+      for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K + i + 1) * C + hxs);
       er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
     }
     PF16 ef;
@@ -1317,20 +1313,19 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, size_t Cx, si
   }
 }
 template <int K>
-__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, size_t Cx, size_t off,
-                                                     const uint64_t* __restrict__ xof,
+__global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk) {
   __shared__ GroupLds lds[GROUPS];
   const int gi = threadIdx.x >> 4;
-  keygen_core_hs<K>(n, C, Cx, off, xof, prf, pk, sk, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
+  keygen_core_hs<K>(n, C, xof, prf, pk, sk, (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
 }
 
 // ------------------------------------------------------------ K-PKE.Encrypt core
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
 template <int K, int MODE, int TW = 64>
-__device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, size_t off, const uint64_t* __restrict__ xof,
+__device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
                                                       const uint8_t* __restrict__ m_base, size_t m_stride,
@@ -1339,10 +1334,9 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
                                                       const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
-  const size_t hl = active ? hs_raw : n - 1;  // index in this launch
-  const size_t hs = off + hl;                 // index in the chunk
+  const size_t hs = active ? hs_raw : n - 1;  // index in the chunk
   const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
-  const size_t hxs = TW == 64 ? hl : 0;  // SampleNTT instance (stride Cx)
+  const size_t hxs = hss;                // SampleNTT instance (stride C)
   const size_t hsm = (TW == 64 || MODE == 0) ? hs : 0;  // m', K', Kbar: LDS on the small decaps path
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
@@ -1370,7 +1364,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   // (profiles/r3/ab_core_arith_c.jsonl).
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * Cx + hxs);
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * C + hxs);
   CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
   // one u-row; LAST: the final row (peeled, so its prefetch is t_hat's words: the core waited on
   // memory 25-29 % of its wave time before, profiles/r2/sq_mlkem768_b20_r2b.txt)
@@ -1385,7 +1379,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
     if (!LAST) {
       if (i + 1 < K) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)((i + 1) * K + j) * Cx + hxs);
+        for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)((i + 1) * K + j) * C + hxs);
       }
     } else {
       // last row: the matrix registers are free, so t_hat's 24 bytes per lane and row (for v
@@ -1469,21 +1463,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, size_t Cx, s
   }
   SS_MARK(TW == 16 && L == 0, 7);
 }
-template <int K, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 4 ? 1 : 3))) void k_encrypt_core(size_t n, size_t C, size_t Cx, size_t off,
-                                                      const uint64_t* __restrict__ xof,
-                                                      const uint64_t* __restrict__ prf,
-                                                      const uint8_t* __restrict__ ek_base, size_t ek_stride,
-                                                      const uint8_t* __restrict__ m_base, size_t m_stride,
-                                                      uint8_t* __restrict__ ct, int32_t* __restrict__ status,
-                                                      const uint64_t* __restrict__ kprime,
-                                                      const uint64_t* __restrict__ kbar, uint8_t* __restrict__ ss) {
-  __shared__ GroupLds lds[GROUPS];
-  const int gi = threadIdx.x >> 4;
-  encrypt_core_hs<K, MODE>(n, C, Cx, off, xof, prf, ek_base, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
-                           (size_t)blockIdx.x * GROUPS + gi, threadIdx.x & 15, lds[gi]);
-}
-
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K, int TW = 64>
 __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
@@ -2227,10 +2206,9 @@ struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
 };
 
 template <int K, int MODE>
-struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and select), 16 lanes / hs,
-                // over the handshakes [off, off + m) of the chunk; xof points at entry `off`
+struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and select), 16 lanes / hs
   static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = K == 4 ? 1 : 3;
-  size_t m, C, off;
+  size_t n, C;
   const uint64_t *xof, *prf;
   const uint8_t* ek;
   size_t ek_stride;
@@ -2243,7 +2221,7 @@ struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and 
   unsigned nb;
   __device__ __forceinline__ void run(unsigned vb, char* lds) const {
     const int gi = threadIdx.x >> 4;
-    encrypt_core_hs<K, MODE>(m, C, C, off, xof, prf, ek, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
+    encrypt_core_hs<K, MODE>(n, C, xof, prf, ek, ek_stride, m_base, m_stride, ct, status, kprime, kbar, ss,
                              (size_t)vb * GROUPS + gi, threadIdx.x & 15, ((GroupLds*)lds)[gi]);
   }
 };
@@ -2261,27 +2239,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(A::WPE > B:
     b.run(tb, lds);
   else
     a.run((uint32_t)w - tb, lds);
-}
-// Three roles: C's workgroups are spread over the grid the same way, A and B share the rest.
-template <class A, class B, class C>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    A::WPE > B::WPE ? (A::WPE > C::WPE ? A::WPE : C::WPE) : (B::WPE > C::WPE ? B::WPE : C::WPE)))) void k_tri(A a, B b,
-                                                                                                            C c) {
-  constexpr int L1 = A::LDS > B::LDS ? A::LDS : B::LDS;
-  constexpr int L = L1 > C::LDS ? L1 : C::LDS;
-  __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
-  const uint64_t N = (uint64_t)a.nb + b.nb + c.nb, w = blockIdx.x;
-  const uint32_t tc = (uint32_t)(w * c.nb / N), tc1 = (uint32_t)((w + 1) * c.nb / N);
-  if (tc1 != tc) {
-    c.run(tc, lds);
-    return;
-  }
-  const uint64_t N2 = (uint64_t)a.nb + b.nb, w2 = w - tc;
-  const uint32_t tb = (uint32_t)(w2 * b.nb / N2), tb1 = (uint32_t)((w2 + 1) * b.nb / N2);
-  if (tb1 != tb)
-    b.run(tb, lds);
-  else
-    a.run((uint32_t)w2 - tb, lds);
 }
 template <class R>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R::WPE))) void k_role(R r) {
@@ -2307,55 +2264,22 @@ void launch_pair(const char* name, const char* name_a, const char* name_b, const
   }
   QRK_LAUNCH(name, st, (k_pair<A, B>), dim3(a.nb + b.nb), dim3(256), 0, st, a, b);
 }
-template <class A, class B, class C>
-void launch_tri(const char* name, const char* name_a, const char* name_b, const char* name_c, const A& a, const B& b,
-                const C& c, const Streams& s) {
-  hipStream_t st = s.main;
-  if (s.serial) {
-    QRK_LAUNCH(name_a, st, k_role<A>, dim3(a.nb), dim3(256), 0, st, a);
-    QRK_LAUNCH(name_b, st, k_role<B>, dim3(b.nb), dim3(256), 0, st, b);
-    QRK_LAUNCH(name_c, st, k_role<C>, dim3(c.nb), dim3(256), 0, st, c);
-    return;
-  }
-  QRK_LAUNCH(name, st, (k_tri<A, B, C>), dim3(a.nb + b.nb + c.nb), dim3(256), 0, st, a, b, c);
-}
 
 // SampleNTT roles for a chunk of C handshakes (n used): the main pass and its fix-up.  The fix-up
 // covers fix-up rates up to 1/64 (~0.7 % expected) in a single pass, one lane per listed entry:
 // it is latency-bound (4+ sequential permutations per lane), a second grid-stride pass would double it.
-// Part q of P (Cq = C / P handshakes, q = 0 / P = 1: the whole chunk) has its own fix-up list and
-// counter, so a part's fix-up can run while the next part's SampleNTT is still filling its list.
 template <int K>
-RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, int q = 0, int P = 1) {
-  const size_t Cq = C / P;
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix + (size_t)q * K * K * Cq, v.nfix + q, (size_t)q * Cq, Cq},
-          blocks_for((size_t)K * K * Cq)};
+RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix}, blocks_for((size_t)K * K * C)};
 }
 template <int K>
-RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, int q = 0, int P = 1) {
-  const size_t Cq = C / P;
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix + (size_t)q * K * K * Cq, v.nfix + q, (size_t)q * Cq, Cq},
-          (unsigned)std::min<size_t>((size_t)K * K * Cq / (64 * 256) + 1, 4096)};
-}
-// the K-PKE.Encrypt role over part q (MODE 0: Encaps, ek = pk, m = coins; MODE 1: the Decaps
-// re-encryption, ek inside dk, m = m'); nb = 0 for a part past the end of the batch
-template <int K, int MODE>
-RCore<K, MODE> core_role(size_t n, size_t C, const ScratchView& v, const uint8_t* ek, size_t ek_stride,
-                         const uint8_t* m_base, size_t m_stride, uint8_t* ct, int32_t* status, uint8_t* ss, int q = 0,
-                         int P = 1) {
-  const size_t Cq = C / P, off = (size_t)q * Cq, m = off < n ? std::min(Cq, n - off) : 0;
-  return {m, C, off, v.xof + off * XOF_W, v.prf, ek, ek_stride, m_base, m_stride, ct, status, v.kprime, v.kbar, ss,
-          (unsigned)((m + GROUPS - 1) / GROUPS)};
+RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
+          (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
 }
 template <class R>
 void launch_one(const char* name, const R& r, const Streams& s) {
   if (r.nb) QRK_LAUNCH(name, s.main, k_role<R>, dim3(r.nb), dim3(256), 0, s.main, r);
-}
-// pipeline parts for a chunk of C handshakes: 0 (no pipeline) unless the schedule asks for one
-// and the parts are whole tiles of the 64-entry layouts
-inline int pipeline_parts(const Streams& s, size_t n, size_t C) {
-  const int P = s.serial ? 1 : s.parts;
-  return (P >= 4 && P <= 16 && C % (64 * (size_t)P) == 0 && n > (size_t)64 * P) ? P : 1;
 }
 
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
@@ -2401,15 +2325,12 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   const auto fx = fix_role<K>(rho, n, C, v);
   QRK_LAUNCH("k_xof_fix", st, (k_role<RXof<K, true>>), dim3(fx.nb), dim3(256), 0, st, fx);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
-             n, C, C, (size_t)0, v.xof, v.prf, pk, sk);
+             n, C, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
 
-// Encaps: rho copy -> {SampleNTT || G(m || H(ek))} -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt.
-// Pipelined (P parts, qrk_ctx_set_streams 2 / 3): launch t runs SampleNTT of part t, the fix-up
-// of part t - 1 and the encrypt core of part t - 2 (plus the front at t = 0, the PRFs at t = 1),
-// so every encrypt-core part but the last shares the chip with VALU-bound Keccak work.
+// Encaps: rho copy -> SampleNTT -> G(m || H(ek)) -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2423,35 +2344,20 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, st);
-  const int NP = pipeline_parts(s, n, C);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4 * NP, st));
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   const RFrontEnc<K> front{pk, coins, n, ss, v.seeds, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
-  auto core = [&](int q) {
-    return core_role<K, 0>(n, C, v, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, nullptr, q, NP);
-  };
-  if (NP == 1) {
-    launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v), front, s);
-    launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix", prf, fix_role<K>(rho, n, C, v), s);
-    launch_one("k_encrypt_core", core(0), s);
-    return hipGetLastError();
-  }
-  launch_pair("k_xof+k_front_encaps", "k_xof", "k_front_encaps", xof_role<K>(rho, n, C, v, 0, NP), front, s);
-  launch_tri("k_xof+k_prf+k_xof_fix", "k_xof", "k_prf", "k_xof_fix", xof_role<K>(rho, n, C, v, 1, NP), prf,
-             fix_role<K>(rho, n, C, v, 0, NP), s);
-  for (int t = 2; t < NP; ++t)
-    launch_tri("k_xof+k_xof_fix+k_encrypt_core", "k_xof", "k_xof_fix", "k_encrypt_core",
-               xof_role<K>(rho, n, C, v, t, NP), fix_role<K>(rho, n, C, v, t - 1, NP), core(t - 2), s);
-  launch_pair("k_xof_fix+k_encrypt_core", "k_xof_fix", "k_encrypt_core", fix_role<K>(rho, n, C, v, NP - 1, NP),
-              core(NP - 2), s);
-  launch_one("k_encrypt_core", core(NP - 1), s);
+  const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
+                         nullptr, (unsigned)((n + GROUPS - 1) / GROUPS)};
+  launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
+  launch_one("k_front_encaps", front, s);
+  launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix", prf, fix_role<K>(rho, n, C, v), s);
+  launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }
 
-// Decaps: rho copy -> {SampleNTT || K-PKE.Decrypt || J(z || c)} -> {G(m' || h) || SampleNTT fix-up}
-// -> PRFs -> re-encryption with the constant-time compare and select.  Pipelined (P parts): launch t
-// runs SampleNTT of part t, the fix-up of part t - 1 and the re-encryption of part t - 3 (plus the
-// decrypt core and J at t = 0, G at t = 1, the PRFs at t = 2).
+// Decaps: rho copy -> SampleNTT -> K-PKE.Decrypt -> J(z || c) -> {G(m' || h) || SampleNTT fix-up}
+// -> PRFs -> re-encryption with the constant-time compare and select
 template <int K>
 hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
                        const Streams& s) {
@@ -2466,37 +2372,19 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, st);
-  const int NP = pipeline_parts(s, n, C);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4 * NP, st));
+  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   const RDecrypt<K> dec{n, ct, sk, v.mprime, gblocks};
   const RJDec<K> jd{ct, sk, n, v.kbar, blocks_for(n)};
   const RGDec<K> gd{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
-  auto core = [&](int q) {
-    return core_role<K, 1>(n, C, v, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
-                           const_cast<uint8_t*>(ct), nullptr, ss, q, NP);
-  };
-  if (NP == 1) {
-    launch_tri("k_xof+k_decrypt_core+k_j_decaps", "k_xof", "k_decrypt_core", "k_j_decaps", xof_role<K>(rho, n, C, v),
-               dec, jd, s);
-    launch_pair("k_g_decaps+k_xof_fix", "k_g_decaps", "k_xof_fix", gd, fix_role<K>(rho, n, C, v), s);
-    launch_one("k_prf", prf, s);
-    launch_one("k_encrypt_core", core(0), s);
-    return hipGetLastError();
-  }
-  launch_tri("k_xof+k_decrypt_core+k_j_decaps", "k_xof", "k_decrypt_core", "k_j_decaps",
-             xof_role<K>(rho, n, C, v, 0, NP), dec, jd, s);
-  launch_tri("k_xof+k_g_decaps+k_xof_fix", "k_xof", "k_g_decaps", "k_xof_fix", xof_role<K>(rho, n, C, v, 1, NP), gd,
-             fix_role<K>(rho, n, C, v, 0, NP), s);
-  launch_tri("k_xof+k_prf+k_xof_fix", "k_xof", "k_prf", "k_xof_fix", xof_role<K>(rho, n, C, v, 2, NP), prf,
-             fix_role<K>(rho, n, C, v, 1, NP), s);
-  for (int t = 3; t < NP; ++t)
-    launch_tri("k_xof+k_xof_fix+k_encrypt_core", "k_xof", "k_xof_fix", "k_encrypt_core",
-               xof_role<K>(rho, n, C, v, t, NP), fix_role<K>(rho, n, C, v, t - 1, NP), core(t - 3), s);
-  launch_pair("k_xof_fix+k_encrypt_core", "k_xof_fix", "k_encrypt_core", fix_role<K>(rho, n, C, v, NP - 1, NP),
-              core(NP - 3), s);
-  launch_one("k_encrypt_core", core(NP - 2), s);
-  launch_one("k_encrypt_core", core(NP - 1), s);
+  const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
+                         const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
+  launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
+  launch_one("k_decrypt_core", dec, s);
+  launch_one("k_j_decaps", jd, s);
+  launch_pair("k_g_decaps+k_xof_fix", "k_g_decaps", "k_xof_fix", gd, fix_role<K>(rho, n, C, v), s);
+  launch_one("k_prf", prf, s);
+  launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }
 

@@ -83,10 +83,6 @@ struct Streams {
   // serial schedule: one kernel per launch (per-kernel timings in isolation); otherwise
   // independent kernels of one operation share multi-role launches (ML-KEM, mlkem.hip)
   bool serial = false;
-  // ML-KEM Encaps / Decaps software pipeline: SampleNTT, its fix-up and the encrypt core in `parts`
-  // parts of the chunk, each launch overlapping one part's core with the next parts' Keccak
-  // (mlkem.hip encaps_impl / decaps_impl); 1: no pipeline
-  int parts = 1;
   // single-shot completion flag (fine-grained host memory, device address): the one-launch ML-KEM
   // kernels store `ticket` there once their outputs are visible to the host
   uint32_t* done = nullptr;

@@ -198,9 +198,8 @@ class BatchKEM:
 
     def set_streams(self, streams: int) -> None:
         """0 (default): independent kernels of one operation share multi-role launches; 1: serial,
-        one kernel per launch (per-kernel timings in isolation); 2 / 3: multi-role launches plus a
-        4- / 8-part SampleNTT / encrypt-core pipeline for batched ML-KEM.  Every kernel runs on
-        the caller's stream in every schedule."""
+        one kernel per launch (per-kernel timings in isolation).  Every kernel runs on the caller's
+        stream in both schedules."""
         self._check(LIB.qrk_ctx_set_streams(self._ctx, streams), "set_streams")
 
     # ------------------------------------------------------------------ kernel timing

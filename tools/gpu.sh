@@ -83,6 +83,27 @@ ab() {
   echo "ab done -> $f"
 }
 
+# abx <rounds> <label>=<tag>[,<bench arg>...] ... -- [common args]: interleaved A/B like ab, where
+# each variant is a library tag (as in ab) plus its own bench arguments (comma-separated), e.g.
+#   abx 3 s0=default s2=default,--streams,2 r3=tree:abtrees/r3head -- --steps 20
+abx() {
+  local rounds=$1; shift
+  local vs=()
+  while [ $# -gt 0 ] && [ "$1" != "--" ]; do vs+=("$1"); shift; done
+  [ $# -gt 0 ] && shift
+  local f=$O/abx.jsonl
+  for r in $(seq 1 "$rounds"); do
+    for v in "${vs[@]}"; do
+      local label=${v%%=*} spec=${v#*=}
+      local tag=${spec%%,*} extra=
+      [ "$spec" != "$tag" ] && extra=${spec#*,}
+      _ab_one "$tag" $(echo "$extra" | tr ',' ' ') "$@" | sed "s/^{\"tag\": \"[^\"]*\"/{\"tag\": \"$label\"/" >> "$f" ||
+        { echo "abx $label failed"; return 1; }
+    done
+  done
+  echo "abx done -> $f"
+}
+
 prof() {
   local tag=$1; shift
   local d=$O/prof_$tag
