@@ -2126,13 +2126,16 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
 
 // ============================================================ multi-role launches
 // Every kernel of a call runs on the caller's stream.  Kernels of one operation that do not depend
-// on each other share one launch instead of running on side streams: a multi-role kernel (k_pair)
-// whose workgroups are interleaved in proportion to the two roles' block counts, so both roles are
-// resident on every CU from the first wave to the last.  That overlaps a latency-bound kernel (the
-// SampleNTT fix-up: ~0.7 % of the entries, 4+ sequential permutations per lane) with a
-// throughput-bound one, and keeps the chip full at mid-size batches, where a lane-per-handshake
-// sponge alone is one wave per SIMD.  A role must not use workgroup barriers (its workgroups may
-// share a launch with another role's) -- the roles below synchronise at most within a wave.
+// on each other share one launch instead of running on side streams: a multi-role kernel
+// (k_multi<A, B, ...>) whose first nb_A workgroups run role A, the next nb_B role B, and so on.
+// The dispatcher hands out workgroups in grid order, so the first role is resident from the start
+// and the later roles fill the CUs around it and after it.  The first role is the latency-bound
+// one: a lane-per-handshake sponge (one wave per SIMD at 2^16 handshakes) or the SampleNTT fix-up
+// (~0.7 % of the entries, 4+ sequential permutations per lane), and the throughput-bound
+// SampleNTT / PRF waves behind it keep the chip full while it runs (tools/fuse_probe.hip,
+// profiles/r4/schedule_probe/: at 2^16 Encaps 0.518 -> 0.475 ms, Decaps 0.598 -> 0.535 ms per
+// call).  A role must not use workgroup barriers (its workgroups may share a CU with another
+// role's) -- the roles below synchronise at most within a wave.
 template <int K, bool FIX>
 struct RXof {  // SampleNTT, lane / matrix entry (FIX: the fix-up list, grid-stride over nb blocks)
   static constexpr int LDS = XOF_LDS, WPE = 1;
@@ -2226,19 +2229,23 @@ struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and 
   }
 };
 
-// Role B takes workgroup w iff floor((w + 1) nb_B / N) > floor(w nb_B / N), N = nb_A + nb_B: the
-// B workgroups are spread evenly over the grid (block-uniform, one scalar division per workgroup).
-template <class A, class B>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(A::WPE > B::WPE ? A::WPE : B::WPE))) void k_pair(
-    A a, B b) {
-  constexpr int L = A::LDS > B::LDS ? A::LDS : B::LDS;
+constexpr int max_of(int a, int b) { return a > b ? a : b; }
+template <class... R>
+struct Roles {
+  static constexpr int LDS = 0, WPE = 1;
+};
+template <class R0, class... R>
+struct Roles<R0, R...> {
+  static constexpr int LDS = max_of(R0::LDS, Roles<R...>::LDS), WPE = max_of(R0::WPE, Roles<R...>::WPE);
+};
+// roles in grid order: workgroup w runs role i with w - (nb_0 + ... + nb_{i-1}) as its block index
+template <class... R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Roles<R...>::WPE))) void k_multi(R... r) {
+  constexpr int L = Roles<R...>::LDS;
   __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
-  const uint64_t N = (uint64_t)a.nb + b.nb, w = blockIdx.x;
-  const uint32_t tb = (uint32_t)(w * b.nb / N), tb1 = (uint32_t)((w + 1) * b.nb / N);
-  if (tb1 != tb)
-    b.run(tb, lds);
-  else
-    a.run((uint32_t)w - tb, lds);
+  unsigned w = blockIdx.x;
+  bool ran = false;
+  ((ran = ran || (w < r.nb ? (r.run(w, lds), true) : (w -= r.nb, false))), ...);
 }
 template <class R>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R::WPE))) void k_role(R r) {
@@ -2252,17 +2259,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(R::WPE))) v
 inline unsigned blocks_for(size_t threads) { return (unsigned)((threads + 255) / 256); }
 inline size_t round64(size_t x) { return (x + 63) & ~(size_t)63; }
 
-// two independent kernels of one operation: one multi-role launch, or (serial schedule) one launch
-// each, A first -- the per-kernel timings in isolation
-template <class A, class B>
-void launch_pair(const char* name, const char* name_a, const char* name_b, const A& a, const B& b, const Streams& s) {
+// independent kernels of one operation: one multi-role launch (roles in grid order), or (serial
+// schedule) one launch each in that order -- the per-kernel timings in isolation.  `name` joins
+// the kernel names with '+'.
+template <class R>
+void launch_one(const char* name, const R& r, const Streams& s) {
+  if (r.nb) QRK_LAUNCH(name, s.main, k_role<R>, dim3(r.nb), dim3(256), 0, s.main, r);
+}
+template <class... R>
+void launch_multi(const char* name, std::initializer_list<const char*> names, const Streams& s, const R&... r) {
   hipStream_t st = s.main;
-  if (s.serial || !a.nb || !b.nb) {
-    if (a.nb) QRK_LAUNCH(name_a, st, k_role<A>, dim3(a.nb), dim3(256), 0, st, a);
-    if (b.nb) QRK_LAUNCH(name_b, st, k_role<B>, dim3(b.nb), dim3(256), 0, st, b);
+  if (s.serial) {
+    const char* const* nm = names.begin();
+    (launch_one(*nm++, r, s), ...);
     return;
   }
-  QRK_LAUNCH(name, st, (k_pair<A, B>), dim3(a.nb + b.nb), dim3(256), 0, st, a, b);
+  const unsigned nb = (0u + ... + r.nb);
+  if (nb) QRK_LAUNCH(name, st, (k_multi<R...>), dim3(nb), dim3(256), 0, st, r...);
 }
 
 // SampleNTT roles for a chunk of C handshakes (n used): the main pass and its fix-up.  The fix-up
@@ -2277,11 +2290,6 @@ RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView
   return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
           (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
 }
-template <class R>
-void launch_one(const char* name, const R& r, const Streams& s) {
-  if (r.nb) QRK_LAUNCH(name, s.main, k_role<R>, dim3(r.nb), dim3(256), 0, s.main, r);
-}
-
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
 inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st) {
   QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho);
@@ -2300,7 +2308,7 @@ void poison_xof(size_t C, const ScratchView& v, hipStream_t st) {
   if (debug_poison()) qrk_chk(hipMemsetAsync(v.xof, 0xFF, (size_t)K * K * C * XOF_W * 8, st));
 }
 
-// KeyGen: front (rho, sigma) -> {SampleNTT || PRFs} -> fix-up -> t_hat rows -> H(ek)
+// KeyGen: front (rho, sigma) -> SampleNTT -> {SampleNTT fix-up, PRFs} -> t_hat rows -> H(ek)
 template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
@@ -2320,17 +2328,16 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
              v.seeds, v.rho);
   const uint8_t* rho = (const uint8_t*)v.rho;
   qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
-  launch_pair("k_xof+k_prf", "k_xof", "k_prf", xof_role<K>(rho, n, C, v),
-              RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)}, s);
-  const auto fx = fix_role<K>(rho, n, C, v);
-  QRK_LAUNCH("k_xof_fix", st, (k_role<RXof<K, true>>), dim3(fx.nb), dim3(256), 0, st, fx);
+  launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
+  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v),
+               RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)});
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
              n, C, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
   return hipGetLastError();
 }
 
-// Encaps: rho copy -> SampleNTT -> G(m || H(ek)) -> {PRFs || SampleNTT fix-up} -> K-PKE.Encrypt
+// Encaps: rho copy -> {G(m || H(ek)), SampleNTT} -> {SampleNTT fix-up, PRFs} -> K-PKE.Encrypt
 template <int K>
 hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, const uint8_t* coins,
                        int32_t* status, void* scratch, const Streams& s) {
@@ -2349,15 +2356,14 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
                          nullptr, (unsigned)((n + GROUPS - 1) / GROUPS)};
-  launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
-  launch_one("k_front_encaps", front, s);
-  launch_pair("k_prf+k_xof_fix", "k_prf", "k_xof_fix", prf, fix_role<K>(rho, n, C, v), s);
+  launch_multi("k_front_encaps+k_xof", {"k_front_encaps", "k_xof"}, s, front, xof_role<K>(rho, n, C, v));
+  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }
 
-// Decaps: rho copy -> SampleNTT -> K-PKE.Decrypt -> J(z || c) -> {G(m' || h) || SampleNTT fix-up}
-// -> PRFs -> re-encryption with the constant-time compare and select
+// Decaps: rho copy -> {J(z || c), K-PKE.Decrypt, SampleNTT} -> G(m' || h) -> {SampleNTT fix-up, PRFs}
+// -> re-encryption with the constant-time compare and select
 template <int K>
 hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* sk, void* scratch,
                        const Streams& s) {
@@ -2379,11 +2385,10 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
-  launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
-  launch_one("k_decrypt_core", dec, s);
-  launch_one("k_j_decaps", jd, s);
-  launch_pair("k_g_decaps+k_xof_fix", "k_g_decaps", "k_xof_fix", gd, fix_role<K>(rho, n, C, v), s);
-  launch_one("k_prf", prf, s);
+  launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
+               xof_role<K>(rho, n, C, v));
+  launch_one("k_g_decaps", gd, s);
+  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }

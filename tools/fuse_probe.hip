@@ -1,5 +1,5 @@
 // Multi-role launches (mlkem.hip k_pair / k_seq): which grouping of the batched ML-KEM-768 Encaps /
-// Decaps kernels is fastest at 2^20 and 2^16 handshakes.  Every variant is the whole launch
+// Decaps kernels is fastest at 2^20, 2^18, 2^16 and 2^14 handshakes.  Every variant is the whole launch
 // sequence of one call after the rho copy; hipEvent timing of 10 back-to-back calls, 5 rounds with
 // the variants interleaved, after a warm-up that brings the clocks up; the median round is printed.
 //   roles alone    xof / front / prf / fix (after its xof) / core / dec / J / G
@@ -11,6 +11,10 @@
 //   D_pair         xof; dec; J; pair(G, fix); prf; core        (round-4 head)
 //   D_seq          seq(J, dec, xof); seq(fix, G); prf; core
 //   D_seq_b        seq(J, xof); dec; seq(fix, G); prf; core
+//   E_m1 / E_m2    seq(front, xof); pair(prf, fix) / xof; front; seq(fix, prf)  (+ core)
+//   D_c            seq(J, xof); seq(fix, dec); G; prf; core
+//   D_d            seq(J, dec, xof); G; seq(fix, prf); core
+//   D_e            seq(J, dec, xof); pair(G, fix); prf; core
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/fuse_probe.hip -o tools/fuse_probe
 #include "../quantum-resistant-p2p_amd/csrc/mlkem.hip"
 
@@ -37,7 +41,21 @@ struct Prio : R {  // the role's waves at the highest wave priority
   }
 };
 
-// role A takes workgroups [0, a.nb), role B the rest
+// the round-4 head's interleaved multi-role kernel: role B takes workgroup w iff
+// floor((w + 1) nb_B / N) > floor(w nb_B / N), N = nb_A + nb_B
+template <class A, class B>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(A::WPE > B::WPE ? A::WPE : B::WPE))) void k_pair(
+    A a, B b) {
+  constexpr int L = A::LDS > B::LDS ? A::LDS : B::LDS;
+  __shared__ __attribute__((aligned(16))) char lds[L > 16 ? L : 16];
+  const uint64_t N = (uint64_t)a.nb + b.nb, w = blockIdx.x;
+  const uint32_t tb = (uint32_t)(w * b.nb / N), tb1 = (uint32_t)((w + 1) * b.nb / N);
+  if (tb1 != tb)
+    b.run(tb, lds);
+  else
+    a.run((uint32_t)w - tb, lds);
+}
+// role A takes workgroups [0, a.nb), role B the rest (as mlkem.hip k_multi)
 template <class A, class B>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(A::WPE > B::WPE ? A::WPE : B::WPE))) void k_seq(
     A a, B b) {
@@ -87,7 +105,9 @@ void fill(void* p, size_t bytes, uint64_t s) {
   hipLaunchKernelGGL(k_fill, dim3((unsigned)((w + 255) / 256)), dim3(256), 0, 0, (uint64_t*)p, w, s);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // optional: one log2 batch size and the number of rounds (default: the four sizes, 5 rounds)
+  const int lb = argc > 1 ? atoi(argv[1]) : 0, rounds = argc > 2 ? atoi(argv[2]) : 5;
   const size_t NMAX = 1 << 20;
   void* scratch;
   uint8_t *pk, *sk, *coins, *ss, *ct;
@@ -106,8 +126,11 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  printf("{\"alg\": \"ML-KEM-768\", \"unit\": \"ms per call (median of 5 rounds of 10)\", \"ms\": {");
-  for (size_t n : {NMAX, (size_t)1 << 16}) {
+  printf("{\"alg\": \"ML-KEM-768\", \"unit\": \"ms per call (median of the rounds of 10 calls)\", \"ms\": {");
+  std::vector<size_t> sizes = {NMAX, (size_t)1 << 18, (size_t)1 << 16, (size_t)1 << 14};
+  if (lb) sizes = {(size_t)1 << lb};
+  bool first = true;
+  for (size_t n : sizes) {
     const size_t C = n;
     ScratchView v = carve(scratch, KK, C);
     fill(v.rho, 32 * n, 3);
@@ -133,6 +156,8 @@ int main() {
         {"memset", [&] { nf(); }},
         {"xof", [&] { nf(); one(xr); }},
         {"xof+fix", [&] { nf(); one(xr); one(fr); }},
+        {"xof_occ4", [&] { nf(); hipLaunchKernelGGL((k_role<RXof<KK, false>>), dim3(xr.nb), dim3(256), 40 * 1024 - XOF_LDS, 0, xr); }},
+        {"xof_occ3", [&] { nf(); hipLaunchKernelGGL((k_role<RXof<KK, false>>), dim3(xr.nb), dim3(256), 53 * 1024 - XOF_LDS, 0, xr); }},
         {"front", [&] { one(front); }},
         {"prf", [&] { one(prf); }},
         {"core", [&] { one(core0); }},
@@ -144,14 +169,19 @@ int main() {
         {"E_pair", [&] { nf(); one(xr); one(front); pair(prf, fr); one(core0); }},
         {"E_seq", [&] { nf(); seq(front, xr); seq(fr, prf); one(core0); }},
         {"E_seq_prio", [&] { nf(); seq(frontp, xr); seq(frp, prf); one(core0); }},
+        {"E_m1", [&] { nf(); seq(front, xr); pair(prf, fr); one(core0); }},
+        {"E_m2", [&] { nf(); one(xr); one(front); seq(fr, prf); one(core0); }},
         {"D_sep", [&] { nf(); one(xr); one(dec); one(jd); one(gd); one(fr); one(prf); one(core1); }},
         {"D_pair", [&] { nf(); one(xr); one(dec); one(jd); pair(gd, fr); one(prf); one(core1); }},
         {"D_seq", [&] { nf(); seq3(jd, dec, xr); seq(fr, gd); one(prf); one(core1); }},
         {"D_seq_b", [&] { nf(); seq(jd, xr); one(dec); seq(fr, gd); one(prf); one(core1); }},
+        {"D_c", [&] { nf(); seq(jd, xr); seq(fr, dec); one(gd); one(prf); one(core1); }},
+        {"D_d", [&] { nf(); seq3(jd, dec, xr); one(gd); seq(fr, prf); one(core1); }},
+        {"D_e", [&] { nf(); seq3(jd, dec, xr); pair(gd, fr); one(prf); one(core1); }},
     };
-    for (int i = 0; i < 10; ++i) vs[11].second();  // warm-up: clocks up
+    for (int i = 0; i < 10; ++i) vs[13].second();  // warm-up: clocks up
     std::vector<std::vector<float>> t(vs.size());
-    for (int r = 0; r < 5; ++r)
+    for (int r = 0; r < rounds; ++r)
       for (size_t j = 0; j < vs.size(); ++j) {
         vs[j].second();
         hipEventRecord(e0, 0);
@@ -162,10 +192,11 @@ int main() {
         hipEventElapsedTime(&ms, e0, e1);
         t[j].push_back(ms / 10);
       }
-    printf("%s\"%zu\": {", n == NMAX ? "" : ", ", n);
+    printf("%s\"%zu\": {", first ? "" : ", ", n);
+    first = false;
     for (size_t j = 0; j < vs.size(); ++j) {
       std::sort(t[j].begin(), t[j].end());
-      printf("%s\"%s\": %.4f", j ? ", " : "", vs[j].first.c_str(), t[j][2]);
+      printf("%s\"%s\": %.4f", j ? ", " : "", vs[j].first.c_str(), t[j][rounds / 2]);
     }
     printf("}");
   }
