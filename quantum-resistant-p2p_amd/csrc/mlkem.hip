@@ -2018,6 +2018,8 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   MkScr& scr = scr_all[hs];
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
+  SS_MARK(blockIdx.x == 0 && lane == 0, 0);
+  SS_MARK(blockIdx.x == NI - 1 && lane == 0, 14);
   {  // (rho, sigma) = G(d || k), in every workgroup
     const uint64_t* d = (const uint64_t*)(coins + hs * 64);
     CState g;
@@ -2028,6 +2030,7 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     if (i >= 0 && i < 4 && coop_canon(c)) sl.rho[i] = cs_word(g);
     if (i >= 4 && i < 8 && coop_canon(c)) sl.sigma[i - 4] = cs_word(g);
     wave_phase();
+    SS_MARK(blockIdx.x == 0 && lane == 0, 13);
   }
   if (item < 2 * K) {  // PRF(sigma, item) -> CBD -> NTT: s_item (operand + dk) or e_(item - K)
     prf_coop<P<K>::ETA1>(sl.sigma, item, sl.ps, c);
@@ -2055,6 +2058,7 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     }
   } else {  // SampleNTT entry e = x K + y straight into the scratch
     xof_coop<K>(sl.rho, item - 2 * K, (uint16_t*)scr.xs, sl.pbuf, c);
+    SS_MARK(item == 2 * K && lane == 0, 15);
   }
   // publish, then count in: the last of the NI workgroups of this handshake finishes it.  With a
   // host-visible completion flag (n == 1, zero-copy pinned outputs) every workgroup's dk stores are
@@ -2072,6 +2076,7 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     return;
   }
   __threadfence();  // acquire: the other workgroups' stores are visible past the counter
+  SS_MARK(lane == 0, 4);
   if ((lane >> 4) < K) {  // t_hat_r = sum_j A[r][j] o s_hat_j + e_hat_r, one 16-lane group per row
     const int r = lane >> 4, L = lane & 15;
     int acc[16];
@@ -2100,6 +2105,7 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     sl.io[48 * K + lane] = sl.rho[lane];
   }
   wave_phase();
+  SS_MARK(lane == 0, 16);
   {  // dk tail: H(ek) || z
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return sl.io[w]; });
@@ -2109,8 +2115,11 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
       tail[i] = cs_word(s);
       tail[4 + i] = z[i];
     }
+    SS_MARK(lane == 0, 17);
   }
-  // wipe the handshake's scratch (s_hat, e_hat, A) and reset its counter for the next call
+  // wipe the handshake's scratch (s_hat, e_hat, A) and reset its counter for the next call (wiping
+  // it before H(ek) instead delays H by 0.9 us and saves 0.4 us after it:
+  // profiles/r4/single_shot/keygen_trace_*.json)
   {
     uint4* w = (uint4*)&scr;
     for (int x = lane; x < (int)(sizeof(MkScr) / 16); x += 64) w[x] = make_uint4(0, 0, 0, 0);
@@ -2118,6 +2127,7 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   if (lane == 0) atomicSub(&cnt[hs], (uint32_t)NI);
   if (done) __threadfence_system();
   mk_wipe_lds(sl);
+  SS_MARK(lane == 0, 18);
   if (done && lane == 0) {
     // n == 1: the only handshake; the flag means every output is visible to the host
     __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -18,7 +18,10 @@ ALG, N = sys.argv[1] if len(sys.argv) > 1 else "ML-KEM-768", 100
 fn = LIB.qrk_dbg_ss_trace
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 MARKS = {
-    "keypair": {13: "G(d||k) done", 14: "wave 0 PRF/NTT + SampleNTT done", 4: "sync", 16: "t rows done", 17: "H(ek) done"},
+    # k_keygen_multi (n = 1): one workgroup per PRF / SampleNTT item, the last to count in finishes
+    "keypair": {14: "last item workgroup started", 13: "G(d||k) done (workgroup 0)",
+                15: "first SampleNTT item done", 4: "last workgroup counted in", 16: "t rows done",
+                17: "H(ek) done", 18: "wipes + system fence done (flag next)"},
     "encaps": {1: "H(ek)+G done", 3: "wave 1 SampleNTT done", 2: "wave 0 PRF + NTT(y_0) done", 4: "sync", 7: "u rows done"},
     "decaps": {8: "decrypt done", 9: "G done", 12: "wave 2 SampleNTT done", 10: "wave 2 PRF done", 4: "rows start",
                11: "J done", 6: "rows done, v + Kbar ready", 7: "select done"},
