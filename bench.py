@@ -172,19 +172,27 @@ def mlkem_core_ops(k, eta1, kind):
     raise ValueError(kind)
 
 
-def kernel_ops_per_hs(alg, name, mode):
+ONE_OP_KERNELS = {"k_front_encaps", "k_j_decaps", "k_g_decaps", "k_decrypt_core", "k_front_decaps"}
+
+
+def kernel_ops_per_hs(alg, name, mode, calls=None):
     """Algorithmic ops one handshake contributes to kernel `name` in one bench step
     (encaps+decaps, or decaps only) and the bound they are priced against.  A multi-role launch
-    ("k_xof+k_front_encaps", mlkem.hip k_pair) carries the sum of its roles' ops (the SampleNTT
-    fix-up, ~0.7 % of the entries, is not counted)."""
+    ("k_front_encaps+k_xof", mlkem.hip k_multi) carries the sum of its roles' ops (the SampleNTT
+    fix-up, ~0.7 % of the entries, is not counted); it runs once per step when one of its roles
+    belongs to Encaps or Decaps alone, so its shared roles (SampleNTT, PRFs) count once then.
+    `calls` overrides how many of the step's operations run a shared kernel."""
     if "+" in name:
-        parts = [kernel_ops_per_hs(alg, p, mode) for p in name.split("+")]
+        roles = name.split("+")
+        c = 1 if any(r in ONE_OP_KERNELS for r in roles) else None
+        parts = [kernel_ops_per_hs(alg, r, mode, c) for r in roles]
         ops = [o for o, _ in parts if o is not None]
         bounds = {b for o, b in parts if o is not None}
         if not ops:
             return None, None
         return sum(ops), (bounds.pop() if len(bounds) == 1 else "valu")
-    calls = 2 if mode == "encdec" else 1  # kernels shared by Encaps and Decaps run once per op
+    if calls is None:
+        calls = 2 if mode == "encdec" else 1  # kernels shared by Encaps and Decaps run once per op
     if alg in HQ:
         wk = hqc_work(alg)
         once = name in ("k_hqc_dec_expand", "k_hqc_decode")  # Decaps-only kernels

@@ -19,10 +19,11 @@ from collections import defaultdict
 from pathlib import Path
 
 
-# ML-KEM multi-role launches (mlkem.hip k_pair / k_tri / k_role): the rocprof name carries the role
-# types; the library's own launch names (QRK_LAUNCH, bench.py's kernel tables) join the roles with '+'
-ROLES = {"RXof<{k}, false>": "k_xof", "RXof<{k}, true>": "k_xof_fix", "RFrontEnc": "k_front_encaps", "RPrf": "k_prf",
-         "RDecrypt": "k_decrypt_core", "RJDec": "k_j_decaps", "RGDec": "k_g_decaps"}
+# ML-KEM role kernels (mlkem.hip k_multi / k_role; k_pair / k_tri in older builds): the rocprof name
+# carries the role types; the library's own launch names (QRK_LAUNCH, bench.py's kernel tables)
+# join the roles with '+'
+ROLES = {"RFrontEnc": "k_front_encaps", "RPrf": "k_prf", "RDecrypt": "k_decrypt_core", "RJDec": "k_j_decaps",
+         "RGDec": "k_g_decaps", "RCore": "k_encrypt_core"}
 
 
 def role_name(t: str) -> str:
@@ -37,7 +38,7 @@ def role_name(t: str) -> str:
 
 
 def short(name: str) -> str:
-    m = re.search(r"(k_pair|k_tri|k_role)<(.*)>\(", name)
+    m = re.search(r"(k_multi|k_pair|k_tri|k_role)<(.*)>\(", name)
     if m:
         args, depth, cur = [], 0, ""
         for ch in m.group(2):

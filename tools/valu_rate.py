@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """Issued VALU op rate per kernel from a tools/pmc_sq.sh pass, against the gfx950 peak.
 
-    tools/valu_rate.py gpurun_out/sq_<tag> <bench line .json> <out.json> [<alg|mode|chunk> key]
+    tools/valu_rate.py gpurun_out/sq_<tag>[,sq_<tag2>] <bench line .json>[,<bench2>] <out.json> [<alg|mode|chunk> key]
+
+Several SQ passes (e.g. the default schedule, whose multi-role launches run several kernels in
+one dispatch, and the serial --streams 1 schedule, one kernel per dispatch) are merged, each with
+the durations of its own bench line: "kernels" (the serial profiled step) or, for the multi-role
+launches, "kernels_timed_region".
 
 With a key, the per-kernel issued rates are also recorded in profiles/valu_rate.json, which
 bench.py reads to add roofline.issued for the same configuration.
@@ -36,9 +41,21 @@ def bench_name(pmc_name: str) -> str:
 
 
 def main() -> None:
-    d, bench_path, out = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
+    dirs = [Path(x) for x in sys.argv[1].split(",")]
+    benches = [Path(x) for x in sys.argv[2].split(",")]
+    out = Path(sys.argv[3])
+    res = {}
+    for d, bench_path in zip(dirs, benches):
+        res.update(one_pass(d, bench_path))
+    summary = {"source": ",".join(map(str, dirs)), "bench": ",".join(map(str, benches)), "peak_Tops": PEAK,
+               "full_rate_ceiling_Tops": FULL_RATE, "kernels": res}
+    finish(summary, res, out)
+
+
+def one_pass(d: Path, bench_path: Path) -> dict:
     bench = json.loads(bench_path.read_text().strip().splitlines()[-1])
-    kernels = bench.get("kernels") or {}
+    kernels = dict(bench.get("kernels_timed_region") or {})
+    kernels.update(bench.get("kernels") or {})
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
     for sub in ("a", "b"):
@@ -69,8 +86,10 @@ def main() -> None:
             r["algorithmic_Tops"] = b["achieved_Tops"]
             r["algorithmic_over_issued"] = b["achieved_Tops"] / issued
         res[k] = r
-    summary = {"source": str(d), "bench": str(bench_path), "peak_Tops": PEAK, "full_rate_ceiling_Tops": FULL_RATE,
-               "kernels": res}
+    return res
+
+
+def finish(summary: dict, res: dict, out: Path) -> None:
     out.write_text(json.dumps(summary, indent=1) + "\n")
     if len(sys.argv) > 4:
         idx = Path(__file__).resolve().parent.parent / "profiles" / "valu_rate.json"
