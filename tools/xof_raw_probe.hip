@@ -17,6 +17,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/xof_raw_probe.hip -o xof_raw_probe
 #include "../quantum-resistant-p2p_amd/csrc/mlkem.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -197,8 +198,22 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  const unsigned gx = (unsigned)((nent + 255) / 256), gc = (unsigned)((nent + 15) / 16);
+  auto ring_l = [&] {
+    hipMemsetAsync(nfix, 0, 4, 0);
+    hipLaunchKernelGGL((k_role<RXof<KK, false>>), dim3(ring.nb), dim3(256), 0, 0, ring);
+  };
+  auto raw_l = [&] {
+    hipMemsetAsync(nfix + 1, 0, 4, 0);
+    hipLaunchKernelGGL(k_xof_raw, dim3(gx), dim3(256), 0, 0, (const uint8_t*)rho, n, C, raw, mask, nfix + 1);
+  };
+  auto load_l = [&] { hipLaunchKernelGGL(k_load, dim3(gc), dim3(256), 0, 0, xof, nent, oa); };
+  auto place_l = [&] { hipLaunchKernelGGL(k_place, dim3(gc), dim3(256), 0, 0, raw, mask, nent, ob); };
+  // warm-up (clocks up, every kernel's code loaded), then 7 rounds with the four kernels
+  // interleaved, 5 launches each; the median round is reported
+  for (int i = 0; i < 20; ++i) ring_l(), raw_l(), load_l(), place_l();
+  std::vector<float> tr, tw, tl, tp;
   auto timeit = [&](auto launch) {
-    launch();  // warm-up
     hipEventRecord(e0, 0);
     for (int i = 0; i < 5; ++i) launch();
     hipEventRecord(e1, 0);
@@ -207,17 +222,22 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     return ms / 5;
   };
-  const unsigned gx = (unsigned)((nent + 255) / 256), gc = (unsigned)((nent + 15) / 16);
-  const float t_ring = timeit([&] {
-    hipMemsetAsync(nfix, 0, 4, 0);
-    hipLaunchKernelGGL((k_role<RXof<KK, false>>), dim3(ring.nb), dim3(256), 0, 0, ring);
-  });
-  const float t_raw = timeit([&] {
-    hipMemsetAsync(nfix + 1, 0, 4, 0);
-    hipLaunchKernelGGL(k_xof_raw, dim3(gx), dim3(256), 0, 0, (const uint8_t*)rho, n, C, raw, mask, nfix + 1);
-  });
-  const float t_load = timeit([&] { hipLaunchKernelGGL(k_load, dim3(gc), dim3(256), 0, 0, xof, nent, oa); });
-  const float t_place = timeit([&] { hipLaunchKernelGGL(k_place, dim3(gc), dim3(256), 0, 0, raw, mask, nent, ob); });
+  for (int r = 0; r < 7; ++r) {
+    tr.push_back(timeit(ring_l));
+    tw.push_back(timeit(raw_l));
+    tl.push_back(timeit(load_l));
+    tp.push_back(timeit(place_l));
+  }
+  auto med = [](std::vector<float> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  const float t_ring = med(tr), t_raw = med(tw), t_load = med(tl), t_place = med(tp);
+  // the outputs compared below come from the last launch of each kernel
+  ring_l();
+  raw_l();
+  load_l();
+  place_l();
   hipMemset(dbg, 0, 16);
   hipLaunchKernelGGL(k_cmp, dim3((unsigned)((nent * 16 + 255) / 256)), dim3(256), 0, 0, oa, ob, mask, nent, dbg, dbg + 1);
   unsigned long long h[2];
