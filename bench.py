@@ -239,6 +239,24 @@ def kernel_ops_per_hs(alg, name, mode, calls=None):
     return None, None
 
 
+def survey_core_ops(alg, name, mode):
+    """SURVEY.md 8d's W terms for an ML-KEM polynomial core, per handshake and step: 896 x 8 ops
+    per NTT or NTT^-1 and 3584 per basemul polynomial (sampling, packing and compare omitted),
+    an independent pricing of the cores next to bench.py's own instruction model."""
+    if alg not in KP:
+        return None
+    k = KP[alg][0]
+    calls = 2 if mode == "encdec" else 1
+    ntt, bm = 896 * 8, 3584
+    if name == "k_encrypt_core":  # NTT(y_j), NTT^-1 of the k u-rows and v; A^T y and t^T y
+        return calls * ((2 * k + 1) * ntt + (k * k + k) * bm)
+    if name == "k_decrypt_core":  # NTT(u_j), NTT^-1(s^T u); s^T u
+        return (k + 1) * ntt + k * bm
+    if name == "k_keygen_core":  # NTT(s_j), NTT(e_i); A s
+        return 2 * k * ntt + k * k * bm
+    return None
+
+
 RED_DEVICE = None  # device of the end-of-run reduction tensors (None = host, for gloo)
 
 
@@ -431,6 +449,9 @@ def kernel_report(alg, mode, prof, B):
             rate = ops * B / (ms * 1e-3)
             peak = {"mfma": MFMA_I8_PEAK, "lds": LDS_LOOKUP_PEAK}.get(bound, VALU_PEAK)
             kernels[name].update(bound=bound, achieved_Tops=rate / 1e12, frac=rate / peak)
+            sw = survey_core_ops(alg, name, mode)
+            if sw is not None:  # the same kernel priced by SURVEY.md 8d's W (NTT + basemul terms only)
+                kernels[name].update(survey_w_Tops=sw * B / (ms * 1e-3) / 1e12, survey_w_frac=sw * B / (ms * 1e-3) / peak)
     roof, mfma = None, None
     if prof:
         dom = max(prof, key=lambda k: prof[k][0])
@@ -557,10 +578,10 @@ def bench_handshake(args, world, rank, local):
     tot = sum(ms for ms, _ in prof.values()) or 1.0
     for name, (ms, cnt) in prof.items():
         kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot}
-    if "k_xof" in prof:  # 4 SampleNTT passes per handshake (2 KeyGen, Encaps, Decaps)
-        k = KP[alg][0]
+    if "k_xof" in prof:  # the 2 KeyGen SampleNTT passes per handshake (Encaps' and Decaps' run
+        k = KP[alg][0]      # inside multi-role launches, mlkem.hip k_multi)
         ms, cnt = prof["k_xof"]
-        ops = 4 * 3 * k * k * PERM_OPS * B * args.steps
+        ops = 2 * 3 * k * k * PERM_OPS * B * args.steps
         roof = {"kernel": "k_xof", "bound": "valu", "achieved": ops / (ms * 1e-3) / 1e12,
                 "peak": VALU_PEAK / 1e12, "unit": "Top/s (int32 lane-ops)",
                 "frac": ops / (ms * 1e-3) / VALU_PEAK, "traffic": None, "avg_launch_ms": ms / cnt,
