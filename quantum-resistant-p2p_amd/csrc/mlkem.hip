@@ -2279,6 +2279,10 @@ void launch_one(const char* name, const R& r, const Streams& s) {
 template <class... R>
 void launch_multi(const char* name, std::initializer_list<const char*> names, const Streams& s, const R&... r) {
   hipStream_t st = s.main;
+  if (names.size() != sizeof...(R)) {  // one name per role (a launcher bug, not an input error)
+    qrk_chk(hipErrorInvalidValue);
+    return;
+  }
   if (s.serial) {
     const char* const* nm = names.begin();
     (launch_one(*nm++, r, s), ...);
