@@ -498,8 +498,10 @@ __device__ __forceinline__ void front_keygen_hs(const uint8_t* __restrict__ coin
 template <int K>
 __global__ __launch_bounds__(256) void k_front_keygen(const uint8_t* __restrict__ coins, size_t n,
                                                       uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
-                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ rho) {
+                                                      uint64_t* __restrict__ seeds, uint64_t* __restrict__ rho,
+                                                      uint32_t* __restrict__ nfix) {
   const size_t hs = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (hs == 0) *nfix = 0;  // the SampleNTT fix-up counter (no memset launch)
   if (hs < n) front_keygen_hs<K>(coins, hs, pk, sk, seeds, rho);
 }
 
@@ -1218,9 +1220,11 @@ inline ScratchView carve(void* base, int K, size_t C) {
 // rho reads at the key stride (1184 B for ML-KEM-768) touch 64 cache lines: rocprofv3 counts
 // 1.2 GB of reads per 2^20-handshake k_xof launch for 33 MB of rho
 // (profiles/r3/rocprof_mlkem768_b20_r3b.json).  The copy is one 32-B read per handshake.
+// It also zeroes the SampleNTT fix-up counter the next kernel counts into (no memset launch).
 __global__ __launch_bounds__(256) void k_rho_copy(const uint8_t* __restrict__ base, size_t stride, size_t n,
-                                                  uint64_t* __restrict__ out) {
+                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ nfix) {
   const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;  // one thread per word
+  if (t == 0) *nfix = 0;
   if (t >= 4 * n) return;
   out[t] = ((const uint64_t*)(base + (t >> 2) * stride))[t & 3];
 }
@@ -2306,7 +2310,8 @@ RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView
 }
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
 inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st) {
-  QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho);
+  QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho,
+             v.nfix);
   return (const uint8_t*)v.rho;
 }
 
@@ -2339,9 +2344,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   }
   hipStream_t st = s.main;
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
-             v.seeds, v.rho);
+             v.seeds, v.rho, v.nfix);
   const uint8_t* rho = (const uint8_t*)v.rho;
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
   launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v),
                RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)});
@@ -2365,7 +2369,6 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, st);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   const RFrontEnc<K> front{pk, coins, n, ss, v.seeds, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
@@ -2392,7 +2395,6 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   poison_xof<K>(C, v, st);
   const uint8_t* rho = rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, st);
-  qrk_chk(hipMemsetAsync(v.nfix, 0, 4, st));
   const RDecrypt<K> dec{n, ct, sk, v.mprime, gblocks};
   const RJDec<K> jd{ct, sk, n, v.kbar, blocks_for(n)};
   const RGDec<K> gd{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(n)};
