@@ -833,6 +833,27 @@ int qrk_ctx_staging_residue(qrk_ctx* ctx, uint64_t out[3]) {
   return 0;
 }
 
+// Tests only (not in qrkem.h): nonzero bytes left in the ML-KEM per-handshake records of a chunk
+// of n handshakes (mlkem_cleanse wipes them after every chunk).
+extern "C" int qrk_dbg_mlkem_records_residue(qrk_ctx* ctx, const char* alg, size_t n, uint64_t* out) {
+  if (!ctx || !out) return fail("null argument");
+  const AlgInfo* a = find_alg(alg);
+  if (!a || a->family != Family::MLKEM) return fail("not an ML-KEM algorithm");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  ctx_quiesce(ctx);
+  size_t off = 0, bytes = 0;
+  mlkem_records_span(*a, (std::min(n, chunk_for(ctx, *a)) + 63) & ~(size_t)63, &off, &bytes);
+  if (off + bytes > ctx->scratch_bytes) return fail("the context's scratch does not cover that chunk");
+  std::vector<uint8_t> tmp(bytes);
+  const hipError_t e = hipMemcpy(tmp.data(), (const char*)ctx->scratch + off, bytes, hipMemcpyDeviceToHost);
+  *out = 0;
+  for (uint8_t x : tmp) *out += x != 0;
+  OQS_MEM_cleanse(tmp.data(), tmp.size());
+  return e == hipSuccess ? 0 : hip_fail("hipMemcpy(records residue)", e);
+}
+
 size_t qrk_ctx_effective_chunk(const qrk_ctx* ctx, const char* alg) {
   const AlgInfo* a = find_alg(alg);
   return (ctx && a) ? chunk_for(ctx, *a) : 0;

@@ -2421,6 +2421,13 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }
 
+void mlkem_records_span(const AlgInfo& a, size_t C, size_t* off, size_t* bytes) {
+  // mlkem::carve: the sampled matrix, the PRF words, then seeds | m' | K' | Kbar (4 C words each)
+  const size_t K = (size_t)a.k;
+  *off = (K * K * C * mlkem::XOF_W + (2 * K + 1) * C * mlkem::PRF_W) * sizeof(uint64_t);
+  *bytes = 16 * C * sizeof(uint64_t);
+}
+
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
   // the one-launch kernels (n <= QRK_SMALL_MAX) keep their key material in LDS and wipe it
   if (n == 0 || n <= QRK_SMALL_MAX) return hipSuccess;

@@ -69,6 +69,9 @@ size_t hqc_scratch_bytes(const AlgInfo& a, size_t chunk);
 // (ML-KEM: seeds, m', K', Kbar; FrodoKEM: seedSE || k || pkh || mu', the hashed key; HQC: the
 // K-hash message m || u || v and m'), stream-ordered: called after every chunk.
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
+// byte offset and length of the ML-KEM per-handshake records (seeds | m' | K' | Kbar) in the
+// scratch of a chunk of C handshakes (tests: qrk_dbg_mlkem_records_residue)
+void mlkem_records_span(const AlgInfo& a, size_t C, size_t* off, size_t* bytes);
 // ML-KEM batches up to this size run as one launch per operation with no scratch key material
 size_t mlkem_small_max();
 // ML-KEM KeyGen batches up to this size run one workgroup per SampleNTT / PRF item (latency)

@@ -119,6 +119,37 @@ def test_os_coins_staging_wiped():
     assert (h, d) == (0, 0)
 
 
+@pytest.mark.parametrize("alg", ["ML-KEM-512", "ML-KEM-768", "ML-KEM-1024"])
+def test_mlkem_records_wiped(alg):
+    """The batched ML-KEM path leaves no per-handshake key material (r / sigma, m', K', Kbar) in
+    scratch once a call has completed (mlkem_cleanse after every chunk, stream-ordered)."""
+    import ctypes as ct
+    from qrkem._native import LIB
+    from qrkem.batch import BatchKEM
+    n = 5000  # batched (above the one-launch sizes), ragged
+    eng = BatchKEM(alg, device=0)
+    fn = LIB.qrk_dbg_mlkem_records_residue
+    fn.argtypes = [ct.c_void_p, ct.c_char_p, ct.c_size_t, ct.POINTER(ct.c_uint64)]
+    out = ct.c_uint64()
+
+    def residue():
+        torch.cuda.synchronize()
+        assert fn(eng._ctx, alg.encode(), n, ct.byref(out)) == 0
+        return out.value
+
+    pk, sk = eng.keypair(n=n)
+    assert residue() == 0
+    ct_, ss = eng.encaps(pk)
+    assert residue() == 0
+    bad = ct_.clone()
+    eng.tamper(bad, seed=5, mode=2)  # implicit rejection selects Kbar for half of them
+    ss2 = eng.decaps(sk, bad)
+    assert residue() == 0
+    flip = (bad != ct_).any(dim=1)
+    assert bool((ss2[~flip] == ss[~flip]).all()) and not bool((ss2[flip] == ss[flip]).all(dim=1).any())
+    eng.close()
+
+
 def test_cleanse_and_device_restore():
     """qrk_ctx_cleanse zeroes the scratch; a call leaves the caller's current device as it was."""
     from qrkem._native import LIB
