@@ -142,14 +142,32 @@ __device__ __forceinline__ uint64_t kword(const KState& s, int i) {
 // Absorb a message of NW 64-bit words (little-endian) produced by `ld(w)`,
 // then pad with domain byte DS at byte offset 8*NW.  RW = rate in words.
 // NW is a compile-time constant so every state index is static.
-// The next block's words are loaded into registers before the current block's
-// permutation runs, so global-load latency hides behind the 24 rounds.
-// (Loading each block's words only when absorbed -- fewer VGPRs, more waves -- was no faster for
-// ML-KEM and slower for the FrodoKEM H(pk) and ss kernels, profiles/r2/ab_absorb_prefetch.jsonl.)
-template <int RW, int NW, uint32_t DS, typename Loader>
+// PF: the next block's words are loaded into registers before the current block's permutation
+// runs, so global-load latency hides behind the 24 rounds (2 x RW VGPRs).  Without PF each block's
+// words are loaded when absorbed: fewer VGPRs, which is what matters where the sponge shares a
+// multi-role launch with SampleNTT (the launch's VGPR budget is the larger role's): the ML-KEM
+// Encaps front and J(z || c) drop from 127 / 130 to 82 / 87 VGPRs and their launches run
+// SampleNTT at 5 waves / SIMD (2^16 handshakes +2.2 %, 2^20 unchanged,
+// profiles/r4/schedule_ab/abx_*_absorb_noprefetch.jsonl).  Alone, prefetching was no slower for
+// ML-KEM and faster for the FrodoKEM H(pk) and ss kernels (profiles/r2/ab_absorb_prefetch.jsonl).
+template <int RW, int NW, uint32_t DS, bool PF = true, typename Loader>
 __device__ __forceinline__ void absorb_words(KState& s, Loader ld) {
   constexpr int NFULL = NW / RW;
   constexpr int TAIL = NW % RW;
+  if constexpr (!PF) {
+#pragma unroll 1
+    for (int b = 0; b < NFULL; ++b) {
+#pragma unroll
+      for (int w = 0; w < RW; ++w) kxor(s, w, ld(b * RW + w));
+      keccak_f(s);
+    }
+#pragma unroll
+    for (int w = 0; w < TAIL; ++w) kxor(s, w, ld(NFULL * RW + w));
+    s.a[TAIL].lo ^= DS;
+    s.a[RW - 1].hi ^= 0x80000000u;
+    keccak_f(s);
+    return;
+  }
   uint64_t nxt[RW];
 #pragma unroll
   for (int w = 0; w < RW; ++w) nxt[w] = (NFULL > 0 || w < TAIL) ? ld(w) : 0;

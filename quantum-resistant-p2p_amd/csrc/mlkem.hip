@@ -535,7 +535,7 @@ __device__ __forceinline__ void front_encaps_hs(const uint8_t* __restrict__ pk, 
   const uint64_t* ek = (const uint64_t*)(pk + hs * P<K>::PK);
   KState s;
   kzero(s);
-  absorb_words<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, [&](int w) { return ek[w]; });
+  absorb_words<RW_SHA3_256, P<K>::PK / 8, DS_SHA3, false>(s, [&](int w) { return ek[w]; });
   uint64_t h[4];
 #pragma unroll
   for (int w = 0; w < 4; ++w) h[w] = kword(s, w);
@@ -572,7 +572,7 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
   const uint64_t* c = (const uint64_t*)(ct + hs * P<K>::CT);
   KState s;
   kzero(s);
-  absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
+  absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE, false>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
 }
