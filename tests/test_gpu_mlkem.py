@@ -261,7 +261,7 @@ def _sample_ntt_needs_4th_block(rho: bytes, i: int, j: int) -> bool:
 
 
 @pytest.mark.parametrize("alg,k,n", [("ML-KEM-768", 3, 1100), ("ML-KEM-512", 2, 1100),
-                                     # half a chunk: ~480 k fix-up entries in one list
+                                     # half a chunk: >= 2^19 entries on one fix-up list
                                      ("ML-KEM-768", 3, (1 << 19) + 3)])
 def test_sample_ntt_fixup_resume_and_overflow(engines, alg, k, n):
     """Every pk of a batch carries a rho whose matrix has entries that need a 4th SHAKE128 block,
