@@ -1257,21 +1257,19 @@ __device__ unsigned long long g_ss_trace[32];
 // ------------------------------------------------------------ KeyGen core
 // s_hat = NTT(CBD(PRF(sigma, j))), e_hat = NTT(CBD(PRF(sigma, k+i))),
 // t_hat_i = sum_j A[i][j] o s_hat_j + e_hat_i   (A[i][j] = SampleNTT(rho || j || i))
-template <int K, int TW = 64>
+template <int K>
 __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                      const uint64_t* __restrict__ prf, uint8_t* __restrict__ pk,
                                                      uint8_t* __restrict__ sk, size_t hs_raw, int L, GroupLds& g) {
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;  // index in the chunk
-  const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
-  const size_t hxs = hss;                // SampleNTT instance (stride C)
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   BOp sb[K];
   {
     CbdRaw sr[K];  // every s_j's CBD words issued before the first NTT
 #pragma unroll
-    for (int j = 0; j < K; ++j) sr[j] = cbd_load<P<K>::ETA1, TW>(prf, (size_t)j * C + hss, L);
+    for (int j = 0; j < K; ++j) sr[j] = cbd_load<P<K>::ETA1, 64>(prf, (size_t)j * C + hs, L);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       PF16 f;
@@ -1288,8 +1286,8 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
   // row i's matrix entries and e_i's CBD words are loaded one row ahead
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K) * C + hxs);
-  CbdRaw er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)K * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(64, (size_t)(j * K) * C + hs);
+  CbdRaw er = cbd_load<P<K>::ETA1, 64>(prf, (size_t)K * C + hs, L);
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
     int acc[16];
@@ -1300,8 +1298,8 @@ __device__ __forceinline__ void keygen_core_hs(size_t n, size_t C, const uint64_
     const CbdRaw ecur = er;
     if (i + 1 < K) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)(j * K + i + 1) * C + hxs);
-      er = cbd_load<P<K>::ETA1, TW>(prf, (size_t)(K + i + 1) * C + hss, L);
+      for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(64, (size_t)(j * K + i + 1) * C + hs);
+      er = cbd_load<P<K>::ETA1, 64>(prf, (size_t)(K + i + 1) * C + hs, L);
     }
     PF16 ef;
     cbd_f<P<K>::ETA1>(ef, ecur);
@@ -1328,7 +1326,7 @@ __global__ __launch_bounds__(256) void k_keygen_core(size_t n, size_t C, const u
 // ------------------------------------------------------------ K-PKE.Encrypt core
 // MODE 0 (encaps): write c.  MODE 1 (decaps): compare c' with the input c and
 // select K' or Kbar in constant time (FIPS 203 Alg. 18 lines 9-11).
-template <int K, int MODE, int TW = 64>
+template <int K, int MODE>
 __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64_t* __restrict__ xof,
                                                       const uint64_t* __restrict__ prf,
                                                       const uint8_t* __restrict__ ek_base, size_t ek_stride,
@@ -1339,9 +1337,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
   const size_t hs = active ? hs_raw : n - 1;  // index in the chunk
-  const size_t hss = TW == 64 ? hs : 0;  // scratch instance (the small path keeps one hs in LDS)
-  const size_t hxs = hss;                // SampleNTT instance (stride C)
-  const size_t hsm = (TW == 64 || MODE == 0) ? hs : 0;  // m', K', Kbar: LDS on the small decaps path
   const uint8_t* ek = ek_base + hs * ek_stride;
   uint8_t* c = ct + hs * P<K>::CT;
   uint32_t diff = 0;
@@ -1350,7 +1345,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   {
     CbdRaw yr[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) yr[j] = cbd_load<P<K>::ETA1, TW>(prf, (size_t)j * C + hss, L);
+    for (int j = 0; j < K; ++j) yr[j] = cbd_load<P<K>::ETA1, 64>(prf, (size_t)j * C + hs, L);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       PF16 f;
@@ -1360,7 +1355,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
       yb[j] = make_bop_f(f, L);
     }
   }
-  SS_MARK(TW == 16 && L == 0, 5);
   // u_i = NTT^-1(sum_j A[j][i] o y_j) + e1_i ;  A[j][i] = SampleNTT(rho || i || j).
   // Row i+1's matrix entries and the next CBD words are loaded one row ahead (latency hidden
   // inside the wave; loading each entry as the basemul needs it, at 4 waves / SIMD, was slower).
@@ -1368,8 +1362,8 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
   // (profiles/r3/ab_core_arith_c.jsonl).
   PK8 an[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)j * C + hxs);
-  CbdRaw er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)K * C + hss, L);
+  for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(64, (size_t)j * C + hs);
+  CbdRaw er = cbd_load<P<K>::ETA2, 64>(prf, (size_t)K * C + hs, L);
   // one u-row; LAST: the final row (peeled, so its prefetch is t_hat's words: the core waited on
   // memory 25-29 % of its wave time before, profiles/r2/sq_mlkem768_b20_r2b.txt)
   auto row = [&](int i, auto last_t) {
@@ -1383,7 +1377,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     if (!LAST) {
       if (i + 1 < K) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(TW, (size_t)((i + 1) * K + j) * C + hxs);
+        for (int j = 0; j < K; ++j) an[j] = LOAD_XOF(64, (size_t)((i + 1) * K + j) * C + hs);
       }
     } else {
       // last row: the matrix registers are free, so t_hat's 24 bytes per lane and row (for v
@@ -1395,7 +1389,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
         an[j].w[0] = a.x, an[j].w[1] = a.y, an[j].w[2] = b.x, an[j].w[3] = b.y, an[j].w[4] = c.x, an[j].w[5] = c.y;
       }
     }
-    er = cbd_load<P<K>::ETA2, TW>(prf, (size_t)(K + i + 1) * C + hss, L);  // e1_{i+1}, or e2 after the last row
+    er = cbd_load<P<K>::ETA2, 64>(prf, (size_t)(K + i + 1) * C + hs, L);  // e1_{i+1}, or e2 after the last row
     PF16 uf;
 #pragma unroll
     for (int t = 0; t < 16; ++t) uf.v[t] = acc_to_f(acc[t]);
@@ -1417,7 +1411,6 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 #pragma unroll 1
   for (int i = 0; i < K - 1; ++i) row(i, std::false_type{});
   row(K - 1, std::true_type{});
-  SS_MARK(TW == 16 && L == 0, 6);
   // v = NTT^-1(t_hat^T o y_hat) + e2 + Decompress_1(m)
   {
     int acc[16];
@@ -1440,7 +1433,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     stride_to_contig_f(vf, (float*)g.poly, L);
     PF16 ef;
     cbd_f<P<K>::ETA2>(ef, er);  // e2
-    const uint8_t* m = m_base + hsm * m_stride;
+    const uint8_t* m = m_base + hs * m_stride;
     const uint32_t mb = (uint32_t)m[2 * L] | ((uint32_t)m[2 * L + 1] << 8);
     P16 v;
 #pragma unroll
@@ -1460,12 +1453,11 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
     const uint32_t d = group_or(diff);
     const uint32_t mask = (uint32_t)(((uint64_t)d - 1u) >> 32);  // all-ones iff d == 0, no branch
     if (L < 8) {
-      const uint32_t kp = ((const uint32_t*)(kprime + hsm * 4))[L];
-      const uint32_t kb = ((const uint32_t*)(kbar + hsm * 4))[L];
+      const uint32_t kp = ((const uint32_t*)(kprime + hs * 4))[L];
+      const uint32_t kb = ((const uint32_t*)(kbar + hs * 4))[L];
       if (active) ((uint32_t*)(ss + hs * 32))[L] = (kp & mask) | (kb & ~mask);
     }
   }
-  SS_MARK(TW == 16 && L == 0, 7);
 }
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K, int TW = 64>
