@@ -105,26 +105,7 @@ constexpr int prep_rowp() { return PREP_HDR + 4 * (N / 8); }
 template <int N>
 constexpr int prep_words() { return prep_rowp<N>() + 4 * N; }
 
-// ---- LDS-replicated T0 lookups.  `tl` = (lane & 31) * 4: the byte offset of this lane's
-// replica column; entry x of the table is at byte 128 x.
-struct Lds {
-  const char* base;  // start of the 32 KiB replicated table
-  uint32_t tl;
-  __device__ __forceinline__ uint32_t at(uint32_t off128) const {  // off128 = 128 * index
-    return *(const uint32_t*)(base + (off128 | tl));
-  }
-  // T_k[byte r of w]
-  __device__ __forceinline__ uint32_t t(int k, uint32_t w, int r) const {
-    const uint32_t off = r == 0 ? (w << 7) & 0x7F80u : (w >> (8 * r - 7)) & 0x7F80u;
-    const uint32_t v = at(off);
-    return k == 0 ? v : k == 1 ? rot8(v) : k == 2 ? rot16(v) : rot24(v);
-  }
-  __device__ __forceinline__ uint32_t sbox(uint32_t w, int r) const {  // S[byte r of w], in byte 1 of T0
-    const uint32_t off = r == 0 ? (w << 7) & 0x7F80u : (w >> (8 * r - 7)) & 0x7F80u;
-    return at(off);
-  }
-};
-
+// ---- LDS-replicated T-table lookups (entry x at byte 256 x; lane slot s = lane & 31).
 // Two replicated tables, T0 and T2 = rot16(T0), interleaved in one 64 KiB array: the 256 B
 // row of entry x holds T0[x] replicated 32 times (bytes 0-127) then T2[x] replicated 32 times
 // (bytes 128-255).  Lane slot s reads byte offset 256 x + 4 s (T0) or 256 x + 128 + 4 s (T2),
@@ -185,53 +166,6 @@ __device__ __forceinline__ void rounds_3_10_x2(const Lds2& L, uint32_t z[4], uin
   }
   round_last2(L, z, rk + 40);
   round_last2(L, w, rk + 40);
-}
-
-// Fill the replicated table (whole workgroup, nthreads threads); caller syncs.
-__device__ __forceinline__ void fill_lds(uint32_t* t32, int tid, int nthreads) {
-  for (int e = tid; e < 256 * 32; e += nthreads) t32[e] = TAB.t0[e >> 5];
-}
-
-// One full round: out_c = T0[b0(s_c)] ^ T1[b1(s_c+1)] ^ T2[b2(s_c+2)] ^ T3[b3(s_c+3)] ^ rk_c
-__device__ __forceinline__ void round_full(const Lds& L, uint32_t s[4], const uint32_t* rk) {
-  uint32_t o[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    o[c] = L.t(0, s[c], 0) ^ L.t(1, s[(c + 1) & 3], 1) ^ L.t(2, s[(c + 2) & 3], 2) ^ L.t(3, s[(c + 3) & 3], 3) ^
-           rk[c];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) s[c] = o[c];
-}
-
-// Final round (no MixColumns): S-box bytes are byte 1 of T0.
-__device__ __forceinline__ void round_last(const Lds& L, uint32_t s[4], const uint32_t* rk) {
-  uint32_t o[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint32_t a = L.sbox(s[c], 0), b = L.sbox(s[(c + 1) & 3], 1), d = L.sbox(s[(c + 2) & 3], 2),
-                   e = L.sbox(s[(c + 3) & 3], 3);
-    o[c] = (((a >> 8) & 0xFFu) | (b & 0xFF00u) | ((d << 8) & 0xFF0000u) | ((e << 16) & 0xFF000000u)) ^ rk[c];
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) s[c] = o[c];
-}
-
-// Rounds 3..10 from the round-2 state z (lane part ^ uniform part); rk = round keys.
-__device__ __forceinline__ void rounds_3_10(const Lds& L, uint32_t z[4], const uint32_t* rk) {
-#pragma unroll
-  for (int r = 3; r < 10; ++r) round_full(L, z, rk + 4 * r);
-  round_last(L, z, rk + 40);
-}
-// Two independent blocks advanced round by round in one basic block: 32 table lookups in
-// flight per round instead of 16 (the kernel is LDS-latency-bound, not bandwidth-bound).
-__device__ __forceinline__ void rounds_3_10_x2(const Lds& L, uint32_t z[4], uint32_t w[4], const uint32_t* rk) {
-#pragma unroll
-  for (int r = 3; r < 10; ++r) {
-    round_full(L, z, rk + 4 * r);
-    round_full(L, w, rk + 4 * r);
-  }
-  round_last(L, z, rk + 40);
-  round_last(L, w, rk + 40);
 }
 
 // row_part below from the constant-memory table (the prep kernel, no LDS table): k = rk0 word 0,

@@ -109,7 +109,6 @@ __device__ __forceinline__ int mont_reduce(int a) {
   const int t = (int)(int16_t)(uint16_t)__umul24((uint32_t)a, (uint32_t)QINV);
   return (a - __mul24(t, Q)) >> 16;
 }
-__device__ __forceinline__ int fqmul(int a, int zm) { return mont_reduce(__mul24(a, zm)); }
 // Barrett to roughly [-q/2, q/2] for |a| < 2^17
 __device__ __forceinline__ int barrett(int a) {
   const int t = (__mul24(a, 20159) + (1 << 25)) >> 26;
@@ -601,129 +600,6 @@ struct GroupLds {
 static_assert(sizeof(GroupLds) / 4 % 32 == 16, "group stride must be 16 mod 32 dwords");
 constexpr int GROUPS = 16;  // 256 threads
 
-__device__ __forceinline__ void stride_to_contig(P16& p, int* buf, int L) {
-#pragma unroll
-  for (int m = 0; m < 16; ++m) buf[L + 17 * m] = p.v[m];
-  gsync();
-#pragma unroll
-  for (int t = 0; t < 16; ++t) p.v[t] = buf[17 * L + t];
-  gsync();
-}
-__device__ __forceinline__ void contig_to_stride(P16& p, int* buf, int L) {
-#pragma unroll
-  for (int t = 0; t < 16; ++t) buf[17 * L + t] = p.v[t];
-  gsync();
-#pragma unroll
-  for (int m = 0; m < 16; ++m) p.v[m] = buf[L + 17 * m];
-  gsync();
-}
-
-// FIPS 203 Alg. 9.  In: stride layout (v[m] = f[L+16m]).  Out: contiguous (v[t] = f[16L+t]).
-__device__ __forceinline__ void ntt_fwd(P16& p, int* buf, int L) {
-#pragma unroll
-  for (int lg = 0; lg < 4; ++lg) {
-    const int step = 8 >> lg;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      if (((m / step) & 1) == 0) {
-        const int zeta = TABC.zm[(1 << lg) + m / (2 * step)];
-        const int t = fqmul(p.v[m + step], zeta);
-        p.v[m + step] = p.v[m] - t;
-        p.v[m] = p.v[m] + t;
-      }
-    }
-  }
-  stride_to_contig(p, buf, L);
-  {
-    const int z = TABD.zm[16 + L];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int u = fqmul(p.v[t + 8], z);
-      p.v[t + 8] = p.v[t] - u;
-      p.v[t] = p.v[t] + u;
-    }
-  }
-  {
-    const int z0 = TABD.zm[32 + 2 * L], z1 = TABD.zm[33 + 2 * L];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (((t >> 2) & 1) == 0) {
-        const int u = fqmul(p.v[t + 4], t < 8 ? z0 : z1);
-        p.v[t + 4] = p.v[t] - u;
-        p.v[t] = p.v[t] + u;
-      }
-    }
-  }
-  {
-    int z[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) z[s] = TABD.zm[64 + 4 * L + s];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (((t >> 1) & 1) == 0) {
-        const int u = fqmul(p.v[t + 2], z[t >> 2]);
-        p.v[t + 2] = p.v[t] - u;
-        p.v[t] = p.v[t] + u;
-      }
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 16; ++t) p.v[t] = barrett(p.v[t]);
-}
-
-// FIPS 203 Alg. 10 (times R, see F_SCALE).  In: contiguous.  Out: stride layout.
-__device__ __forceinline__ void ntt_inv(P16& p, int* buf, int L) {
-  {
-    int z[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) z[s] = TABD.zm[127 - 4 * L - s];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (((t >> 1) & 1) == 0) {
-        const int x = p.v[t], y = p.v[t + 2];
-        p.v[t] = x + y;
-        p.v[t + 2] = fqmul(y - x, z[t >> 2]);
-      }
-    }
-  }
-  {
-    const int z0 = TABD.zm[63 - 2 * L], z1 = TABD.zm[62 - 2 * L];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      if (((t >> 2) & 1) == 0) {
-        const int x = p.v[t], y = p.v[t + 4];
-        p.v[t] = x + y;
-        p.v[t + 4] = fqmul(y - x, t < 8 ? z0 : z1);
-      }
-    }
-  }
-  {
-    const int z = TABD.zm[31 - L];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int x = p.v[t], y = p.v[t + 8];
-      p.v[t] = x + y;
-      p.v[t + 8] = fqmul(y - x, z);
-    }
-  }
-  contig_to_stride(p, buf, L);
-#pragma unroll
-  for (int lg = 3; lg >= 0; --lg) {
-    const int step = 8 >> lg;  // len/16 for len = 16 << (3 - lg)
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      if (((m / step) & 1) == 0) {
-        const int zeta = TABC.zm[(2 << lg) - 1 - m / (2 * step)];
-        const int x = p.v[m], y = p.v[m + step];
-        p.v[m] = x + y;
-        p.v[m + step] = fqmul(y - x, zeta);
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < 16; ++m) p.v[m] = fqmul(p.v[m], F_SCALE);
-}
-
 // ---- fp32 NTTs (plain domain).  Same data movement as the integer versions above.
 struct PF16 {
   float v[16];
@@ -887,17 +763,6 @@ struct BOp {  // basemul right operand
 
 __device__ __forceinline__ uint32_t pack16(int lo, int hi) {
   return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
-}
-
-__device__ __forceinline__ BOp make_bop(const P16& b, int L) {
-  BOp r;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int g = fqmul(b.v[2 * u + 1], TABD.gm[8 * L + u]);
-    r.b0[u] = pack16(b.v[2 * u], g);
-    r.b1[u] = pack16(b.v[2 * u + 1], b.v[2 * u]);
-  }
-  return r;
 }
 
 // From an fp32 NTT output (|b| <= 11658, fits int16): B0 = (b0, b1 gamma mod q),
