@@ -32,14 +32,12 @@ namespace qrk {
 namespace mlkem {
 
 constexpr int Q = 3329;
-constexpr int QINV = 62209;  // q^-1 mod 2^16
 // The batched SampleNTT output holds 12-bit coefficients (384 B per matrix entry, 8 per 12-byte
 // chunk) rather than int16 (512 B): the encrypt core waits on memory, not on the VALU (SQ wait_any
 // 0.28-0.35 after the round-3 arithmetic cut its VALU instructions 20 % with no change in time), and
 // the matrix is 58 % of its HBM reads.
 constexpr int XOF_W = 48;    // u64 words per matrix entry in scratch
 constexpr int PRF_W = 24;    // up to 192 B of PRF output (eta = 3)
-constexpr int F_SCALE = 1441;  // 128^-1 * R^2 mod q  (undoes invNTT length and one R^-1)
 
 // ---------------------------------------------------------------- tables
 constexpr int powq(int b, int e) {
@@ -57,20 +55,6 @@ constexpr int centered(long x) {
   if (x < 0) x += Q;
   return (int)(x > Q / 2 ? x - Q : x);
 }
-struct Tables {
-  int zm[128];  // zeta_i * R mod q (centered): Montgomery-form NTT twiddles
-  int gm[128];  // gamma_i * R mod q: basemul moduli X^2 - gamma_i
-};
-constexpr Tables make_tables() {
-  Tables t{};
-  for (int i = 0; i < 128; ++i) {
-    t.zm[i] = centered((long)powq(17, br7(i)) * 65536);
-    t.gm[i] = centered((long)powq(17, 2 * br7(i) + 1) * 65536);
-  }
-  return t;
-}
-constexpr Tables TABC = make_tables();          // compile-time indexed twiddles
-__constant__ Tables TABD = make_tables();       // lane-indexed twiddles
 
 // Plain-domain twiddles as fp32 (centered integers, exact): the NTTs run in fp32.  zq is z
 // divided by q (rounded to fp32) for the three-FMA modular product below.
@@ -102,21 +86,6 @@ __device__ __forceinline__ int sign_mask(int x) {
   int r;
   asm("v_ashrrev_i32 %0, 31, %1" : "=v"(r) : "v"(x));
   return r;
-}
-// Signed Montgomery reduction, R = 2^16: returns a * R^-1 mod q, |r| < 2^15 + q/2.
-// 4 full-rate VALU ops: v_mul_u32_u24, v_bfe_i32, v_mad_i32_i24, v_ashrrev.
-__device__ __forceinline__ int mont_reduce(int a) {
-  const int t = (int)(int16_t)(uint16_t)__umul24((uint32_t)a, (uint32_t)QINV);
-  return (a - __mul24(t, Q)) >> 16;
-}
-// Barrett to roughly [-q/2, q/2] for |a| < 2^17
-__device__ __forceinline__ int barrett(int a) {
-  const int t = (__mul24(a, 20159) + (1 << 25)) >> 26;
-  return a - __mul24(t, Q);
-}
-__device__ __forceinline__ int canon(int a) {
-  const int r = barrett(a);
-  return r + ((r >> 31) & Q);
 }
 // ---- fp32 modular arithmetic (every value is an exact integer below 2^24)
 // MAGIC = 1.5 * 2^23: x + MAGIC rounds x to an integer (round-to-nearest-even), and
@@ -1397,12 +1366,11 @@ __device__ __forceinline__ void wave_phase() {
 
 // SampleNTT entry e = x K + y (FIPS 203 Alg. 7) on one wave: SHAKE128(rho || x || y) squeezed
 // block by block; each block's 56 byte triples are parsed by lanes 0-55 (two candidates each)
-// and the accepted ones placed by ballot prefix counts, so the wave keeps FIPS order.  Output:
-// coefficient j of entry e at int16 index ((j / 8) 16 + e) 8 + j % 8 of xs16 (the k_xof layout at
-// tile width 16).  pbuf: this wave's 44-dword LDS parse buffer.
-template <int K>
-__device__ __forceinline__ void xof_coop(const uint64_t* __restrict__ rho, int e, uint16_t* __restrict__ xs16,
-                                         uint32_t* __restrict__ pbuf, const Coop& c) {
+// and the accepted ones placed by ballot prefix counts, so the wave keeps FIPS order:
+// place(j, value) for coefficient j.  pbuf: this wave's 44-dword LDS parse buffer.
+template <int K, typename Place>
+__device__ __forceinline__ void xof_coop_place(const uint64_t* __restrict__ rho, int e, uint32_t* __restrict__ pbuf,
+                                               const Coop& c, Place place) {
   const int i = c.idx, lane = threadIdx.x & 63;
   CState s;
   if (i >= 0 && i < 4) cs_xor(s, rho[i]);
@@ -1429,11 +1397,38 @@ __device__ __forceinline__ void xof_coop(const uint64_t* __restrict__ rho, int e
     const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0)) +
                     (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m2, 0));
     const int p1 = cnt + pre, p2 = p1 + (a1 ? 1 : 0);
-    if (a1 && p1 < 256) xs16[(((p1 >> 3) * 16 + e) << 3) + (p1 & 7)] = (uint16_t)d1;
-    if (a2 && p2 < 256) xs16[(((p2 >> 3) * 16 + e) << 3) + (p2 & 7)] = (uint16_t)d2;
+    if (a1 && p1 < 256) place(p1, d1);
+    if (a2 && p2 < 256) place(p2, d2);
     cnt += __popcll(m1) + __popcll(m2);
     wave_phase();  // this block's parse reads are done before the next block's pbuf writes
   }
+}
+// ... into the single-shot layout: coefficient j of entry e at int16 index ((j / 8) 16 + e) 8 + j % 8
+// of xs16 (the k_xof layout at tile width 16)
+template <int K>
+__device__ __forceinline__ void xof_coop(const uint64_t* __restrict__ rho, int e, uint16_t* __restrict__ xs16,
+                                         uint32_t* __restrict__ pbuf, const Coop& c) {
+  xof_coop_place<K>(rho, e, pbuf, c,
+                    [&](int j, uint32_t d) { xs16[(((j >> 3) * 16 + e) << 3) + (j & 7)] = (uint16_t)d; });
+}
+// ... into the batched layout (the SampleNTT fix-up for small chunks, one wave per listed entry
+// inst = xy C + hs): the 256 values in FIPS order in the wave's LDS buffer cb, then lanes 0-31
+// pack one 8-coefficient chunk each into the entry's 12-bit tiles, as k_xof would have
+template <int K>
+__device__ __forceinline__ void xof_fix_coop(const uint8_t* __restrict__ rho_base, size_t rho_stride, size_t C,
+                                             uint32_t inst, XUnit* __restrict__ out, uint16_t* __restrict__ cb,
+                                             uint32_t* __restrict__ pbuf, const Coop& c) {
+  const size_t hs = inst % C;
+  xof_coop_place<K>((const uint64_t*)(rho_base + hs * rho_stride), (int)(inst / C), pbuf, c,
+                    [&](int j, uint32_t d) { cb[j] = (uint16_t)d; });
+  const int lane = threadIdx.x & 63;
+  if (lane < 32) {
+    uint32_t r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = cb[8 * lane + j];
+    chunk_store(xc<XTW>(xent<XTW>(out, inst), lane), r);
+  }
+  wave_phase();  // cb is read before the next entry's values are placed
 }
 
 // PRF instance N on one wave: SHAKE256(seed || N) -> 64 eta bytes; word w at ps[w 16 + N].
