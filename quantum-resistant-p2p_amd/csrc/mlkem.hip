@@ -2009,6 +2009,25 @@ struct RXof {  // SampleNTT, lane / matrix entry (FIX: the fix-up list, grid-str
   unsigned nb;
   __device__ __forceinline__ void run(unsigned vb, char* lds) const { xof_body<K, FIX>(a, vb, nb, (uint32_t*)lds); }
 };
+// The fix-up list on one wave per entry (small chunks): the wave-cooperative sponge (~2.7 us per
+// permutation) instead of one lane's (~9 us on a lone wave), so the 4+ dependent permutations of an
+// entry stop being the critical path of the launch
+template <int K>
+struct RXofFixCoop {
+  static constexpr int WAVE_LDS = 512 + 44 * 4;  // 256 placed values (u16) + the parse buffer
+  static constexpr int LDS = 4 * WAVE_LDS, WPE = 1;
+  XofArgs<K, true> a;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+    const int wave = threadIdx.x >> 6;
+    char* w = lds + wave * WAVE_LDS;
+    const Coop c = coop_init();
+    const uint32_t limit = *a.nfix;
+#pragma unroll 1
+    for (uint32_t r = vb * 4 + wave; r < limit; r += nb * 4)  // wave-uniform
+      xof_fix_coop<K>(a.rho_base, a.rho_stride, a.C, a.fix[r], a.out, (uint16_t*)w, (uint32_t*)(w + 512), c);
+  }
+};
 template <int K>
 struct RFrontEnc {  // (K, r) = G(m || H(ek)), lane / handshake
   static constexpr int LDS = 0, WPE = 1;
@@ -2160,6 +2179,26 @@ RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView
   return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
           (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
 }
+// chunks up to this size run the fix-up one wave per entry (RXofFixCoop): below it the
+// lane-per-entry fix-up's latency shows past the PRFs it shares a launch with, above it the
+// cooperative form's issue slots (~4x per entry) cost more.  Same-box A/Bs against the lane form
+// (profiles/r4/schedule_ab/abx_2p1*_coop_fixup.jsonl): 2^13 +24.8 %, 2^14 +15.8 %, 2^15 +4.5 %,
+// 2^16 -3.1 %, 2^17 -4.2 %.
+constexpr size_t COOP_FIX_MAX = (size_t)1 << 15;
+template <int K>
+RXofFixCoop<K> fix_coop_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
+  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
+          (unsigned)std::min<size_t>((size_t)K * K * C / 256 + 1, 4096)};  // waves for 1/64 of the entries
+}
+// {SampleNTT fix-up, PRFs}: the fix-up's workgroups first (grid order)
+template <int K, class Prf>
+void launch_fix_prf(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, const Prf& prf, const Streams& s) {
+  if (C <= COOP_FIX_MAX)
+    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_coop_role<K>(rho, n, C, v), prf);
+  else
+    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
+}
+
 // k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
 inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st) {
   QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho,
@@ -2199,8 +2238,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
              v.seeds, v.rho, v.nfix);
   const uint8_t* rho = (const uint8_t*)v.rho;
   launch_one("k_xof", xof_role<K>(rho, n, C, v), s);
-  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v),
-               RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)});
+  launch_fix_prf<K>(rho, n, C, v, RPrf<P<K>::ETA1, P<K>::ETA1>{v.seeds, n, C, 2 * K, 2 * K, v.prf, blocks_for(2 * K * C)},
+                    s);
   QRK_LAUNCH("k_keygen_core", st, k_keygen_core<K>, dim3((unsigned)((n + GROUPS - 1) / GROUPS)), dim3(256), 0, st,
              n, C, v.xof, v.prf, pk, sk);
   QRK_LAUNCH("k_back_keygen", st, k_back_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk);
@@ -2226,7 +2265,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
                          nullptr, (unsigned)((n + GROUPS - 1) / GROUPS)};
   launch_multi("k_front_encaps+k_xof", {"k_front_encaps", "k_xof"}, s, front, xof_role<K>(rho, n, C, v));
-  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
+  launch_fix_prf<K>(rho, n, C, v, prf, s);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }
@@ -2256,7 +2295,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
                xof_role<K>(rho, n, C, v));
   launch_one("k_g_decaps", gd, s);
-  launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
+  launch_fix_prf<K>(rho, n, C, v, prf, s);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
 }
