@@ -10,16 +10,20 @@
 // independent Keccak instances, each run by one lane, and polynomial stages,
 // each run by a 16-lane group per handshake.
 //
-//   k_front_*  lane / handshake   H(ek), G(.), J(z||c)             (SHA3 / SHAKE256)
-//   k_prf      lane / (nonce, hs)  PRF_eta(seed, N) raw bytes      (SHAKE256)
-//   k_xof      lane / (x, y, hs)   SampleNTT raw XOF blocks        (SHAKE128, 3-4 blocks)
-//   k_keygen_core / k_encrypt_core / k_decrypt_core
-//              16 lanes / hs       CBD, rejection compaction, NTT, basemul, invNTT,
-//                                  compress/encode, FO re-encrypt compare + implicit rejection
+//   front / J / G  lane / handshake   H(ek), G(.), J(z||c)            (SHA3 / SHAKE256)
+//   PRFs           lane / (nonce, hs)  PRF_eta(seed, N) raw bytes     (SHAKE256)
+//   SampleNTT      lane / (x, y, hs)   3 SHAKE128 blocks, compacted to 12-bit chunks in the
+//                                      producer; the ~0.7 % of entries that need a 4th block
+//                                      go on a fix-up list (lane or wave per entry)
+//   keygen / encrypt / decrypt cores
+//                  16 lanes / hs       CBD, NTT, basemul, invNTT, compress/encode,
+//                                      FO re-encrypt compare + implicit rejection
 //
-// Raw Keccak output goes to device scratch in a 64-instance tiled SoA layout
-// (word w of instance i at ((i/64)*W + w)*64 + i%64): every lane-per-instance
-// store is a fully coalesced 512-byte wave store.
+// Independent stages of one operation share multi-role launches (k_multi, roles in grid order,
+// every kernel on the caller's stream); n <= 1024 runs one-launch kernels with wave-cooperative
+// sponges instead (the reference's one-call-per-handshake pattern).  Keccak output goes to device
+// scratch in a 64-instance tiled SoA layout (word w of instance i at ((i/64)*W + w)*64 + i%64):
+// every lane-per-instance store is a fully coalesced 512-byte wave store.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
