@@ -146,8 +146,12 @@ __device__ __forceinline__ uint64_t cs_get(const CState& s, int w) {
   const int a = 4 * coop_lane_of(w);
   return ((uint64_t)bperm(a, s.hi) << 32) | bperm(a, s.lo);
 }
-// the permutation as a call (one copy of the unrolled rounds per kernel, not one per call site)
-static __device__ __noinline__
+// The permutation inlined at every call site.  As a call (one copy per kernel) every entry began
+// with s_waitcnt vmcnt(0) lgkmcnt(0), which waited for the caller's outstanding stores and
+// prefetch loads before the first round; inlined, the waits sit at the uses: ML-KEM-768 OQS
+// keypair / encaps / decaps 56.6 / 55.4 / 44.2 -> 54.2 / 53.8 / 42.9 us, FrodoKEM-640-AES
+// single calls -6 % (profiles/r4/single_shot/*_coop_call_vs_inline.jsonl).
+static __device__ __forceinline__
 CState kf_coop(CState s, Coop c) {
   keccak_f_coop(s.lo, s.hi, c);
   return s;
