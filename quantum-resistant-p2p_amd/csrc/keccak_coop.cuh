@@ -9,7 +9,7 @@
 //
 // Layout: row y of the state in lanes 8y .. 8y + 7, lane 8y + s holding column
 // (s + 4) mod 5 -- columns 0-4 at slots 1-5 plus replicas of columns 4, 0, 1 at slots 0, 6, 7 --
-// as a lo/hi pair; lanes 40-63 are idle.  Per round:
+// as a lo/hi pair; lanes 40-47, 48-55 and 56-63 mirror row 4.  Per round:
 //   theta : column parity = XOR over the rows: DPP row_ror:8, then v_permlane16_swap and
 //           v_permlane32_swap butterflies; C[x-1] / C[x+1] are the neighbouring slots (DPP
 //           row_shr:1 / row_shl:1), so theta needs no LDS round trip
@@ -18,7 +18,11 @@
 //           straight from the canonical lanes pi moves them from (ds_bpermute), then a ^ (~b & c)
 //   iota  : the (0, 0) lane and its replica
 // Replicas absorb the same message words as their canonical lane, so they mirror it at every
-// round start.
+// round start.  The three row-4 mirrors replace a column-parity mask: the first butterfly step
+// leaves lanes 32-47 unpaired (row 4 twice) and pairs 48-55 with 56-63 (row 4 ^ row 4 = 0), so no
+// lane needs masking and each round's chain is one instruction shorter: 6478 -> 6364 cycles per
+// permutation alone, ML-KEM-768 single-shot calls -0.35 to -0.6 us
+// (profiles/r4/single_shot/{coop_probe,latency}_mirror_rows_ab.*).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,14 +41,14 @@ namespace qrk {
 // inside the kernel.
 
 struct Coop {
-  int idx;          // state index x + 5y held by this lane (replica lanes too), or -1 for an idle lane
+  int idx;          // state index x + 5y held by this lane (replica lanes too)
   int a_m1, a_p1;   // zero (round-1 layout fields; kept so kf_coop's argument layout is unchanged)
   int g0, g1, g2;   // ds_bpermute byte addresses of the chi inputs B[X][Y], B[X+1][Y], B[X+2][Y]
   uint32_t shift;   // rho: v_alignbit shift (32 - r mod 32) mod 32
   bool swap;        // rho: swap the halves first
   uint32_t m0;      // all-ones where iota applies (lane (0, 0) and its replica)
-  uint32_t live;    // all-ones on the 40 state lanes (the column parity ignores the rest)
   bool hi_slots;    // slots 6, 7 (refreshed from slots 1, 2)
+  uint32_t hsm;     // all-ones on slots 6, 7
 };
 
 // v2: lane s + 8y (slot s = 0..7 of row y) holds column x(s) = (s + 4) mod 5: columns 0-4 at slots
@@ -57,29 +61,25 @@ __device__ __forceinline__ Coop coop_init() {
   constexpr uint8_t RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
   Coop c;
   const int l = threadIdx.x & 63;
-  const int sl = l & 7, y = l >> 3;
-  const bool v = y < 5;
+  const int sl = l & 7, y = (l >> 3) < 4 ? (l >> 3) : 4;  // lanes 40-63: three mirrors of row 4
   const int x = (sl + 4) % 5;
-  c.idx = v ? x + 5 * y : -1;
+  c.idx = x + 5 * y;
   c.a_m1 = c.a_p1 = 0;
   auto lane_xy = [](int xx, int yy) { return 4 * (xx + 1 + 8 * yy); };
   const int X0 = x, X1 = (x + 1) % 5, X2 = (x + 2) % 5, Y = y;
-  c.g0 = v ? lane_xy((3 * Y + X0) % 5, X0) : 4 * l;
-  c.g1 = v ? lane_xy((3 * Y + X1) % 5, X1) : 4 * l;
-  c.g2 = v ? lane_xy((3 * Y + X2) % 5, X2) : 4 * l;
-  c.live = v ? 0xFFFFFFFFu : 0u;
-  c.m0 = (v && sl == 1 && y == 0) ? 0xFFFFFFFFu : 0u;  // the replica at slot 6 is refreshed from slot 1
+  c.g0 = lane_xy((3 * Y + X0) % 5, X0);
+  c.g1 = lane_xy((3 * Y + X1) % 5, X1);
+  c.g2 = lane_xy((3 * Y + X2) % 5, X2);
+  c.m0 = (sl == 1 && y == 0) ? 0xFFFFFFFFu : 0u;  // the replica at slot 6 is refreshed from slot 1
   c.hi_slots = sl >= 6;
-  const int r = v ? RHO[x + 5 * y] : 0;
+  c.hsm = sl >= 6 ? 0xFFFFFFFFu : 0u;
+  const int r = RHO[x + 5 * y];
   const int n = r & 31;
   c.shift = (uint32_t)((32 - n) & 31);
   c.swap = (r >= 32) != (n == 0);  // alignbit by 0 returns the low operand: r = 0 needs the swap
   return c;
 }
 
-__device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) {  // lane l <- lane (l + 8) mod 16 of its row
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, true);
-}
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t v) {  // lane l <- lane l - 1 (same row)
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
 }
@@ -92,17 +92,24 @@ __device__ __forceinline__ uint32_t dpp_shl2(uint32_t v) {  // lane l <- lane l 
 __device__ __forceinline__ uint32_t dpp_shr5(uint32_t v) {  // lane l <- lane l - 5 (same row)
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x115, 0xF, 0xF, true);
 }
+// a DPP shift (CTRL) with the 16-lane rows whose ROWS bit is clear left at 0 (0x128: row_ror:8)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_rows(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, true);
+}
 __device__ __forceinline__ uint32_t bperm(int addr, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v); }
 
 // 24 rounds on the wave's state (lo, hi of this lane's A[x][y]); every lane of the wave calls it.
 __device__ __forceinline__ void keccak_f_coop(uint32_t& lo, uint32_t& hi, const Coop& c) {
+  // sl_ / sh_: copies of lo / hi that the first butterfly step overwrites in place (the next
+  // round's come out of the slot refresh as a v_bitop3 select beside the v_cndmask one)
+  uint32_t sl_ = lo, sh_ = hi;
 #pragma unroll 24
   for (int r = 0; r < 24; ++r) {
-    // column parity over the 8 rows (rows 5-7 and idle lanes masked): pairs within a 16-lane
-    // row (DPP row_ror:8), then across rows (permlane swaps); every lane ends with C[x(s)]
-    uint32_t cl = lo & c.live, ch = hi & c.live;
-    cl ^= dpp_ror8(cl);
-    ch ^= dpp_ror8(ch);
+    // column parity over the rows: pairs within a 16-lane row (DPP row_ror:8) for rows 0-3, while
+    // lanes 32-47 keep row 4 (16-lane row 2 masked) and lanes 48-63 (two copies of row 4) cancel
+    // to zero; then across rows (permlane swaps); every lane ends with C[x(s)]
+    uint32_t cl = sl_ ^ dpp_rows<0x128, 0xB>(sl_), ch = sh_ ^ dpp_rows<0x128, 0xB>(sh_);
     // lo and hi share the cross-row butterflies: swap16(cl, ch) leaves rows 0/2 with lo pair sums
     // and rows 1/3 with hi pair sums; swap32 completes them; a last swap16 hands every lane both.
     // Each swap takes two registers holding the same sum: the second copy is a v_bitop3 XOR
@@ -131,6 +138,8 @@ __device__ __forceinline__ void keccak_f_coop(uint32_t& lo, uint32_t& hi, const 
     lo = (b0l ^ (~b1l & b2l)) ^ (KRC_LO[r] & c.m0);
     hi = (b0h ^ (~b1h & b2h)) ^ (KRC_HI[r] & c.m0);
     const uint32_t rl = dpp_shr5(lo), rh = dpp_shr5(hi);
+    sl_ = __builtin_amdgcn_bitop3_b32(c.hsm, rl, lo, 0xCA);  // hsm ? rl : lo
+    sh_ = __builtin_amdgcn_bitop3_b32(c.hsm, rh, hi, 0xCA);
     lo = c.hi_slots ? rl : lo;
     hi = c.hi_slots ? rh : hi;
   }
