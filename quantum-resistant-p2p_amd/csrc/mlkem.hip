@@ -1773,6 +1773,9 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
   SS_MARK(threadIdx.x == 0, 0);
+  // z (dk's last 32 bytes) is loaded with d: the coins row may be host memory (single-shot calls),
+  // and a load after H(ek) put one more PCIe round trip on the critical path
+  const uint64_t zw = (wave == 0 && i >= 0 && i < 4) ? ((const uint64_t*)(coins + hs * 64 + 32))[i] : 0;
   if (wave == 0) {  // (rho, sigma) = G(d || k)
     const uint64_t* d = (const uint64_t*)(coins + hs * 64);
     CState g;
@@ -1821,10 +1824,9 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return ekw[w]; });
     uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
-    const uint64_t* z = (const uint64_t*)(coins + hs * 64 + 32);
     if (i >= 0 && i < 4) {
       tail[i] = cs_word(s);
-      tail[4 + i] = z[i];
+      tail[4 + i] = zw;
     }
     SS_MARK(threadIdx.x == 0, 17);
   }
@@ -1878,6 +1880,9 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   MkScr& scr = scr_all[hs];
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
+  // z for dk's tail, loaded with d (one PCIe round trip when coins is host memory) rather than
+  // after H(ek) in the last workgroup
+  const uint64_t zw = (i >= 0 && i < 4) ? ((const uint64_t*)(coins + hs * 64 + 32))[i] : 0;
   SS_MARK(blockIdx.x == 0 && lane == 0, 0);
   SS_MARK(blockIdx.x == NI - 1 && lane == 0, 14);
   {  // (rho, sigma) = G(d || k), in every workgroup
@@ -1970,10 +1975,9 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     CState s;
     coop_absorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, c, [&](int w) { return sl.io[w]; });
     uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
-    const uint64_t* z = (const uint64_t*)(coins + hs * 64 + 32);
     if (i >= 0 && i < 4 && coop_canon(c)) {
       tail[i] = cs_word(s);
-      tail[4 + i] = z[i];
+      tail[4 + i] = zw;
     }
     SS_MARK(lane == 0, 17);
   }
