@@ -26,6 +26,7 @@
 // every lane-per-instance store is a fully coalesced 512-byte wave store.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "keccak.cuh"
@@ -1865,8 +1866,11 @@ __device__ __forceinline__ void mk_wipe_lds(MkLds& sl) {
   for (int x = threadIdx.x; x < (int)(sizeof(MkLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
 }
 
+struct KgCoins {  // one handshake's KeyGen coins d || z passed by value (single-shot host calls)
+  uint64_t w[8];
+};
 template <int K>
-__global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __restrict__ coins,
+__global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __restrict__ coins, KgCoins cv,
                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
                                                      MkScr* __restrict__ scr_all, uint32_t* __restrict__ cnt,
                                                      uint32_t* done, uint32_t ticket) {
@@ -1880,13 +1884,14 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   MkScr& scr = scr_all[hs];
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
-  // z for dk's tail, loaded with d (one PCIe round trip when coins is host memory) rather than
-  // after H(ek) in the last workgroup
-  const uint64_t zw = (i >= 0 && i < 4) ? ((const uint64_t*)(coins + hs * 64 + 32))[i] : 0;
+  // the coins row: the kernel argument (n == 1 host calls: no PCIe read before G) or memory; z for
+  // dk's tail is loaded with d rather than after H(ek) in the last workgroup
+  const uint64_t* cw = coins ? (const uint64_t*)(coins + hs * 64) : cv.w;
+  const uint64_t zw = (i >= 0 && i < 4) ? cw[4 + i] : 0;
   SS_MARK(blockIdx.x == 0 && lane == 0, 0);
   SS_MARK(blockIdx.x == NI - 1 && lane == 0, 14);
   {  // (rho, sigma) = G(d || k), in every workgroup
-    const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+    const uint64_t* d = cw;
     CState g;
     if (i >= 0 && i < 4) cs_xor(g, d[i]);
     if (i == 4) g.lo ^= (uint32_t)K | (DS_SHA3 << 8);
@@ -2232,8 +2237,14 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
+    KgCoins cv{};
+    const bool by_value = n == 1 && s.host_coins;
+    if (by_value) memcpy(cv.w, s.host_coins, sizeof(cv.w));
     QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
-               s.main, n, coins, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
+               s.main, n, by_value ? nullptr : coins, cv, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr,
+               s.ticket);
+    volatile uint64_t* vw = cv.w;  // the host copy of the coins does not outlive the launch call
+    for (int w = 0; w < 8; ++w) vw[w] = 0;
     return hipGetLastError();
   }
   if (n <= QRK_SMALL_MAX) {
