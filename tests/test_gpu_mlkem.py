@@ -32,10 +32,11 @@ def _host(t):
 
 
 @pytest.mark.parametrize("alg", ALGS)
-@pytest.mark.parametrize("n", [1, 17, 255, 256, 257, 301, 1024, 1025])
+@pytest.mark.parametrize("n", [1, 2, 16, 17, 255, 256, 257, 301, 1024, 1025])
 def test_roundtrip_matches_oracle(engines, alg, n):
-    """n <= 256 runs the one-launch small-batch kernels (k_*_small), n > 256 the batched
-    schedule; both byte-exact vs the oracle, including the boundary."""
+    """n <= 1024 runs the one-launch small-batch kernels (KeyGen: one workgroup per item for
+    n <= 16, k_keygen_multi, then one per handshake), n > 1024 the batched schedule; both
+    byte-exact vs the oracle, including the boundaries."""
     import oracle as orc
     eng = engines[alg]
     coins = orc.bench_coins(n, 96, seed=1234 + n)
