@@ -142,7 +142,7 @@ struct qrk_ctx {
   uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
-  const uint8_t* hcoins_next = nullptr;  // ... and, for a KeyGen, its coins row in host memory
+  const uint8_t* hin_next[2] = {nullptr, nullptr};  // ... and the inputs' host copies (by-value kernel args)
   hipStream_t io_stream = nullptr;
   int streams = 0;            // 0: multi-role launches, 1: serial (one kernel per launch)
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
@@ -362,7 +362,8 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
-    S.host_coins = ctx->hcoins_next;
+    S.host_in1 = ctx->hin_next[0];
+    S.host_in2 = ctx->hin_next[1];
   }
   if (a.family == Family::MLKEM && op == Op::KEYPAIR && n <= mlkem_kg_multi_max()) {
     if (!ctx->kg_cnt) {
@@ -490,13 +491,14 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   if (spin) {
     ctx->ticket = ctx->ticket + 1 ? ctx->ticket + 1 : 1;
     ctx->flag_next = true;
-    ctx->hcoins_next = op == Op::KEYPAIR && l_i1 ? h : nullptr;
+    ctx->hin_next[0] = l_i1 ? h : nullptr;
+    ctx->hin_next[1] = l_i2 ? h + o_i2 : nullptr;
   }
   // ML-KEM decapsulation reports no status (implicit rejection): only encapsulation writes it
   int rc = run_batch(ctx, a, op, n, d + o_o1, l_o2 ? d + o_o2 : nullptr, l_i1 ? d : nullptr, l_i2 ? d + o_i2 : nullptr,
                      (status && op == Op::ENCAPS) ? (int32_t*)(d + o_st) : nullptr, st);
   ctx->flag_next = false;
-  ctx->hcoins_next = nullptr;
+  ctx->hin_next[0] = ctx->hin_next[1] = nullptr;
   hipError_t e = hipSuccess;
   if (!rc && spin) {
     // bounded spin; a kernel that never stores the ticket (a launch or execution error) falls

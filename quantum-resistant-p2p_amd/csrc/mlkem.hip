@@ -1611,8 +1611,13 @@ __device__ __forceinline__ bool enc_v_one(const OneLds& sl, const uint8_t* __res
 }
 
 template <int K>
+struct EncIn {  // one handshake's Encaps inputs passed by value (single-shot host calls)
+  uint64_t pk[P<K>::PK / 8], coins[4];
+};
+template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const uint8_t* __restrict__ pk,
-                                                                const uint8_t* __restrict__ coins, uint8_t* __restrict__ ct,
+                                                                const uint8_t* __restrict__ coins, EncIn<K> in,
+                                                                uint8_t* __restrict__ ct,
                                                                 uint8_t* __restrict__ ss, int32_t* __restrict__ status,
                                                                 uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
@@ -1623,8 +1628,9 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   constexpr int EKW = P<K>::PK / 8;
   SS_MARK(threadIdx.x == 0, 0);
   SS_CLK(threadIdx.x == 0, 20);
-  stage_in(sl.io, (const uint64_t*)(pk + hs * P<K>::PK), EKW);
-  stage_in(sl.io + EKW, (const uint64_t*)(coins + hs * 32), 4);
+  // inputs from memory, or (pk == nullptr: n == 1 host calls) from the kernel argument
+  stage_in(sl.io, pk ? (const uint64_t*)(pk + hs * P<K>::PK) : in.pk, EKW);
+  stage_in(sl.io + EKW, pk ? (const uint64_t*)(coins + hs * 32) : in.coins, 4);
   __syncthreads();
   const uint64_t* ek = sl.io;
   if (wave == 0) {  // (K, r) = G(m || H(ek)): the critical chain
@@ -1669,9 +1675,20 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   wipe_one(sl, done, ticket);
 }
 
+// one handshake's Decaps inputs passed by value (single-shot host calls; ML-KEM-1024's 4.6 KB would
+// exceed the 4 KB of kernel arguments, so it keeps the pointer path)
+template <int K, bool FITS = (P<K>::CT + P<K>::SK <= 3584)>
+struct DecIn {
+  uint64_t ct[P<K>::CT / 8], sk[P<K>::SK / 8];
+};
+template <int K>
+struct DecIn<K, false> {
+  uint64_t ct[1], sk[1];
+};
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const uint8_t* __restrict__ ct,
-                                                                const uint8_t* __restrict__ sk, uint8_t* __restrict__ ss,
+                                                                const uint8_t* __restrict__ sk, DecIn<K> in,
+                                                                uint8_t* __restrict__ ss,
                                                                 uint32_t* done, uint32_t ticket) {
   __shared__ __attribute__((aligned(16))) OneLds sl;
   const size_t hs = blockIdx.x;
@@ -1679,8 +1696,9 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
   const Coop c = coop_init();
   const int i = c.idx;
   constexpr int CTW = P<K>::CT / 8, SKW = P<K>::SK / 8;
-  stage_in(sl.io, (const uint64_t*)(ct + hs * P<K>::CT), CTW);
-  stage_in(sl.io + CTW, (const uint64_t*)(sk + hs * P<K>::SK), SKW);
+  // inputs from memory, or (ct == nullptr: n == 1 host calls) from the kernel argument
+  stage_in(sl.io, ct ? (const uint64_t*)(ct + hs * P<K>::CT) : in.ct, CTW);
+  stage_in(sl.io + CTW, ct ? (const uint64_t*)(sk + hs * P<K>::SK) : in.sk, SKW);
   uint8_t* cc = (uint8_t*)sl.io;                   // the received ciphertext (LDS copy)
   const uint8_t* dk = (const uint8_t*)(sl.io + CTW);  // dk (LDS copy)
   constexpr int XW = ONE_WAVES - 3;  // SampleNTT waves 2 .. ONE_WAVES - 2; the last wave computes v
@@ -2238,8 +2256,8 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
     KgCoins cv{};
-    const bool by_value = n == 1 && s.host_coins;
-    if (by_value) memcpy(cv.w, s.host_coins, sizeof(cv.w));
+    const bool by_value = n == 1 && s.host_in1;
+    if (by_value) memcpy(cv.w, s.host_in1, sizeof(cv.w));
     QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
                s.main, n, by_value ? nullptr : coins, cv, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr,
                s.ticket);
@@ -2272,8 +2290,16 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_encaps_one", s.main, k_encaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, pk,
-               coins, ct, ss, status, n == 1 ? s.done : nullptr, s.ticket);
+    EncIn<K> in{};
+    const bool by_value = n == 1 && s.host_in1 && s.host_in2;
+    if (by_value) {
+      memcpy(in.pk, s.host_in1, sizeof(in.pk));
+      memcpy(in.coins, s.host_in2, sizeof(in.coins));
+    }
+    QRK_LAUNCH("k_encaps_one", s.main, k_encaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n,
+               by_value ? nullptr : pk, coins, in, ct, ss, status, n == 1 ? s.done : nullptr, s.ticket);
+    volatile uint64_t* vc = in.coins;  // the host copy of the coins does not outlive the launch call
+    for (int w = 0; w < 4; ++w) vc[w] = 0;
     return hipGetLastError();
   }
   hipStream_t st = s.main;
@@ -2297,8 +2323,19 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
-    QRK_LAUNCH("k_decaps_one", s.main, k_decaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n, ct, sk,
-               ss, n == 1 ? s.done : nullptr, s.ticket);
+    DecIn<K> in{};
+    constexpr bool FITS = sizeof(in.ct) == P<K>::CT;
+    const bool by_value = FITS && n == 1 && s.host_in1 && s.host_in2;
+    if constexpr (FITS) {
+      if (by_value) {
+        memcpy(in.ct, s.host_in1, sizeof(in.ct));
+        memcpy(in.sk, s.host_in2, sizeof(in.sk));
+      }
+    }
+    QRK_LAUNCH("k_decaps_one", s.main, k_decaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n,
+               by_value ? nullptr : ct, sk, in, ss, n == 1 ? s.done : nullptr, s.ticket);
+    volatile uint64_t* vs = in.sk;  // the host copy of the secret key does not outlive the launch call
+    for (size_t w = 0; w < sizeof(in.sk) / 8; ++w) vs[w] = 0;
     return hipGetLastError();
   }
   hipStream_t st = s.main;

@@ -93,9 +93,10 @@ struct Streams {
   // per-handshake arrival counters of the multi-workgroup single-shot ML-KEM KeyGen (device,
   // QRK_KG_MULTI_MAX words, zero between calls: the last workgroup of a handshake resets its word)
   uint32_t* kg_cnt = nullptr;
-  // single-shot KeyGen (n == 1, host-pointer call): the coins row in host memory; the kernel takes
-  // its 64 bytes as a kernel argument instead of reading them over PCIe
-  const uint8_t* host_coins = nullptr;
+  // single-shot ML-KEM (n == 1, host-pointer call): the inputs in host memory (KeyGen: coins;
+  // Encaps: pk, coins); the kernel takes them as a kernel argument instead of reading them over PCIe
+  const uint8_t* host_in1 = nullptr;
+  const uint8_t* host_in2 = nullptr;
 };
 
 // All pointers are device pointers; n handshakes processed as one chunk
