@@ -1675,9 +1675,10 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   wipe_one(sl, done, ticket);
 }
 
-// one handshake's Decaps inputs passed by value (single-shot host calls; ML-KEM-1024's 4.6 KB would
-// exceed the 4 KB of kernel arguments, so it keeps the pointer path)
-template <int K, bool FITS = (P<K>::CT + P<K>::SK <= 3584)>
+// one handshake's Decaps inputs passed by value (single-shot host calls): up to ML-KEM-1024's 4736 B,
+// past the 4 KB of kernel arguments often quoted -- a 4800-byte argument launches and reads back
+// correctly on this stack (tools/kernarg_probe.hip, profiles/r4/single_shot/kernarg_probe_4800B.txt)
+template <int K, bool FITS = (P<K>::CT + P<K>::SK <= 4736)>
 struct DecIn {
   uint64_t ct[P<K>::CT / 8], sk[P<K>::SK / 8];
 };
