@@ -69,13 +69,22 @@ def is_kem_enabled(alg_name: str) -> bool:
     return bool(LIB.OQS_KEM_alg_is_enabled(alg_name.encode()))
 
 
+_SIZES: dict = {}
+
+
 def kem_sizes(alg_name: str) -> dict:
+    # constants per mechanism, read from the library once (the reference's call pattern builds a
+    # new KeyEncapsulation per encaps / decaps, so this sits on every single-shot call)
+    hit = _SIZES.get(alg_name)
+    if hit is not None:
+        return dict(hit)
     out = (ct.c_size_t * 6)()
     if LIB.qrk_kem_sizes(alg_name.encode(), out) != 0:
         raise MechanismNotSupportedError(alg_name)
     keys = ("length_public_key", "length_secret_key", "length_ciphertext",
             "length_shared_secret", "length_keypair_coins", "length_encaps_coins")
-    return dict(zip(keys, (int(v) for v in out)))
+    _SIZES[alg_name] = dict(zip(keys, (int(v) for v in out)))
+    return dict(_SIZES[alg_name])
 
 
 class _KemPrefix(ct.Structure):
@@ -92,6 +101,9 @@ def _fixed(data: Union[bytes, bytearray, memoryview], size: int) -> ct.Array:
     return ct.create_string_buffer(bytes(data), size)
 
 
+_ATTRS: dict = {}  # mechanism -> the handle struct's fields (constant per mechanism)
+
+
 class KeyEncapsulation:
     """One KEM mechanism; mirrors ``oqs.KeyEncapsulation`` (oqs.py:227-393)."""
 
@@ -104,19 +116,27 @@ class KeyEncapsulation:
         self._kem = LIB.OQS_KEM_new(alg_name.encode())
         if not self._kem:
             raise RuntimeError(f"OQS_KEM_new({alg_name}) failed: {last_error()}")
-        # every attribute comes from the handle's struct, as oqs.py:273-280 reads it
-        k = ct.cast(self._kem, ct.POINTER(_KemPrefix)).contents
-        sz = kem_sizes(alg_name)
-        self._kp_coins = sz["length_keypair_coins"]
-        self._enc_coins = sz["length_encaps_coins"]
-        self.method_name = k.method_name
-        self.alg_version = k.alg_version
-        self.claimed_nist_level = int(k.claimed_nist_level)
-        self.ind_cca = int(k.ind_cca)
-        self.length_public_key = int(k.length_public_key)
-        self.length_secret_key = int(k.length_secret_key)
-        self.length_ciphertext = int(k.length_ciphertext)
-        self.length_shared_secret = int(k.length_shared_secret)
+        # every attribute comes from the handle's struct, as oqs.py:273-280 reads it; the struct is
+        # the same for every handle of a mechanism, so it is read once per mechanism (the reference's
+        # call pattern builds a new object per encaps / decaps: ~3 us of ctypes field reads each)
+        attrs = _ATTRS.get(alg_name)
+        if attrs is None:
+            k = ct.cast(self._kem, ct.POINTER(_KemPrefix)).contents
+            sz = kem_sizes(alg_name)
+            attrs = {
+                "_kp_coins": sz["length_keypair_coins"],
+                "_enc_coins": sz["length_encaps_coins"],
+                "method_name": k.method_name,
+                "alg_version": k.alg_version,
+                "claimed_nist_level": int(k.claimed_nist_level),
+                "ind_cca": int(k.ind_cca),
+                "length_public_key": int(k.length_public_key),
+                "length_secret_key": int(k.length_secret_key),
+                "length_ciphertext": int(k.length_ciphertext),
+                "length_shared_secret": int(k.length_shared_secret),
+            }
+            _ATTRS[alg_name] = attrs
+        self.__dict__.update(attrs)
         self.details = {
             "name": alg_name,
             "version": self.alg_version.decode(),
