@@ -123,12 +123,14 @@ int qrk_ctx_cleanse(qrk_ctx *ctx);
  * OS-drawn coins (coins == NULL) to the device, wiped before every call returns -- and in the
  * first 64 MiB of device scratch (out[2], zero after qrk_ctx_cleanse). */
 int qrk_ctx_staging_residue(qrk_ctx *ctx, uint64_t out[3]);
-/* Handshakes per chunk actually used for `alg` (FrodoKEM caps the chunk so its
- * scratch stays near 8 GiB); 0 for an unknown algorithm. */
+/* Handshakes per chunk actually used for `alg` (FrodoKEM and HQC cap the chunk so their
+ * scratch stays within QRK_SCRATCH_GIB = 48 GiB); 0 for an unknown algorithm. */
 size_t qrk_ctx_effective_chunk(const qrk_ctx *ctx, const char *alg);
 /* Schedule of one operation's kernels, all on the caller's stream: 0 (default): independent
- * kernels share multi-role launches (their workgroups interleaved in one grid); 1: serial, one
- * kernel per launch (kernel timings in isolation).  Any other value: QRK_EINVAL. */
+ * kernels share multi-role launches (each role's workgroups a contiguous range of one grid, in
+ * grid order); 1: serial, one kernel per launch (kernel timings in isolation).  Any other value
+ * returns -1 with qrk_last_error() set.  (Round 3's value 2, the forked split pipeline, was
+ * removed in round 4 and is rejected now.) */
 int qrk_ctx_set_streams(qrk_ctx *ctx, int streams);
 
 /* Sizes of `alg`: out[0..5] = pk, sk, ct, ss, keypair coin bytes, encaps coin bytes. */

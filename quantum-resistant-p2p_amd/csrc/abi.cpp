@@ -149,7 +149,7 @@ struct qrk_ctx {
   hipStream_t last_stream = nullptr;  // ... on this stream
   bool last_valid = false;
   hipEvent_t ev_up = nullptr;    // end of the OS-coin upload (run_batch)
-  std::mutex mu;
+  mutable std::mutex mu;
 };
 
 // Calls that use a context's scratch are ordered one after another whatever stream each runs
@@ -810,6 +810,7 @@ int qrk_ctx_set_streams(qrk_ctx* ctx, int streams) {
 
 int qrk_ctx_set_chunk(qrk_ctx* ctx, size_t chunk) {
   if (!ctx || chunk == 0) return fail("bad chunk");
+  std::lock_guard<std::mutex> lk(ctx->mu);  // chunk_for reads it under the lock
   ctx->chunk = (chunk + 63) & ~(size_t)63;
   return 0;
 }
@@ -862,7 +863,9 @@ extern "C" int qrk_dbg_mlkem_records_residue(qrk_ctx* ctx, const char* alg, size
 
 size_t qrk_ctx_effective_chunk(const qrk_ctx* ctx, const char* alg) {
   const AlgInfo* a = find_alg(alg);
-  return (ctx && a) ? chunk_for(ctx, *a) : 0;
+  if (!ctx || !a) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return chunk_for(ctx, *a);
 }
 
 int qrk_ctx_profile(qrk_ctx* ctx, int enable) {

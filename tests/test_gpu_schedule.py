@@ -37,8 +37,7 @@ def _rows_per_part(a, b, n=N, parts=PARTS):
 
 
 @pytest.mark.parametrize("alg,n", [("ML-KEM-768", N), ("ML-KEM-1024", N),
-                                   # a full-chunk batch (>= mlkem.hip BIG_CHUNK), ragged: the grouping
-                                   # the library picks for large chunks
+                                   # a ragged batch of more than 2^19 handshakes in one chunk
                                    ("ML-KEM-768", (1 << 19) + 4097)])
 def test_back_to_back_auto_vs_serial(alg, n):
     """KeyGen -> Encaps -> tamper -> Decaps on one context with no host synchronisation in

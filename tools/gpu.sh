@@ -85,7 +85,7 @@ ab() {
 
 # abx <rounds> <label>=<tag>[,<bench arg>...] ... -- [common args]: interleaved A/B like ab, where
 # each variant is a library tag (as in ab) plus its own bench arguments (comma-separated), e.g.
-#   abx 3 s0=default s2=default,--streams,2 r3=tree:abtrees/r3head -- --steps 20
+#   abx 3 s0=default s1=default,--streams,1 r3=tree:abtrees/r3head -- --steps 20
 abx() {
   local rounds=$1; shift
   local vs=()
