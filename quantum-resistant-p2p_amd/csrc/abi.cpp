@@ -19,6 +19,22 @@
 #include "../../include/qrkem.h"
 #include "qrkem_internal.h"
 
+// -DQRK_HOST_TRACE=1 (tools/build_variant.sh builds only): steady-clock stamps at the phases of a
+// single-shot call, read by qrk_dbg_host_trace (tools/host_trace.py)
+#ifndef QRK_HOST_TRACE
+#define QRK_HOST_TRACE 0
+#endif
+#if QRK_HOST_TRACE
+static long long g_host_trace[16];
+#define HT(i) (g_host_trace[i] = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count())
+extern "C" int qrk_dbg_host_trace(long long* out) {
+  memcpy(out, g_host_trace, sizeof(g_host_trace));
+  return 0;
+}
+#else
+#define HT(i) ((void)0)
+#endif
+
 namespace qrk {
 
 // ------------------------------------------------------------------ algorithm table
@@ -142,7 +158,7 @@ struct qrk_ctx {
   uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
-  const uint8_t* hin_next[2] = {nullptr, nullptr};  // ... and the inputs' host copies (by-value kernel args)
+  const uint8_t* hin_next = nullptr;  // ... and the public input's host copy (a by-value kernel argument)
   hipStream_t io_stream = nullptr;
   int streams = 0;            // 0: multi-role launches, 1: serial (one kernel per launch)
   hipEvent_t ev_last = nullptr;  // recorded at the end of the last call that used the scratch
@@ -362,18 +378,18 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
   if (ctx->flag_next) {
     S.done = ctx->hflag_dev;
     S.ticket = ctx->ticket;
-    S.host_in1 = ctx->hin_next[0];
-    S.host_in2 = ctx->hin_next[1];
+    S.host_in1 = ctx->hin_next;
   }
   if (a.family == Family::MLKEM && op == Op::KEYPAIR && n <= mlkem_kg_multi_max()) {
     if (!ctx->kg_cnt) {
-      hipError_t e = hipMalloc((void**)&ctx->kg_cnt, mlkem_kg_multi_max() * sizeof(uint32_t));
-      if (e == hipSuccess) e = hipMemset(ctx->kg_cnt, 0, mlkem_kg_multi_max() * sizeof(uint32_t));
+      hipError_t e = hipMalloc((void**)&ctx->kg_cnt, mlkem_kg_flag_words() * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipMemset(ctx->kg_cnt, 0, mlkem_kg_flag_words() * sizeof(uint32_t));
       if (e != hipSuccess) return hip_fail("hipMalloc(kg_cnt)", e);
     }
     S.kg_cnt = ctx->kg_cnt;
   }
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
+  HT(3);
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     hipError_t e = hipSuccess;
@@ -430,6 +446,7 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
           break;
       }
     }
+    HT(4);
     if (e == hipSuccess) e = g_launch_err;
     if (e != hipSuccess) return hip_fail("kernel launch", e);
     // key material of this chunk (seeds, m', K', Kbar, ...) does not outlive the call
@@ -484,6 +501,7 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
     else if (os_random(h + o_i2, n * l_i2)) return -1;
   }
   memset(h + o_st, 0, n * sizeof(int32_t));
+  HT(2);
   uint8_t* d = ctx->hio_dev;
   // n == 1: the kernel stores a ticket in fine-grained pinned memory once its outputs are visible,
   // and the host spins on it (about 4 us sooner than hipStreamSynchronize wakes up)
@@ -491,14 +509,15 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   if (spin) {
     ctx->ticket = ctx->ticket + 1 ? ctx->ticket + 1 : 1;
     ctx->flag_next = true;
-    ctx->hin_next[0] = l_i1 ? h : nullptr;
-    ctx->hin_next[1] = l_i2 ? h + o_i2 : nullptr;
+    // the public input (Encaps pk, Decaps c) may travel as a kernel argument; KeyGen's coins never
+    ctx->hin_next = (op != Op::KEYPAIR && l_i1) ? h : nullptr;
   }
   // ML-KEM decapsulation reports no status (implicit rejection): only encapsulation writes it
   int rc = run_batch(ctx, a, op, n, d + o_o1, l_o2 ? d + o_o2 : nullptr, l_i1 ? d : nullptr, l_i2 ? d + o_i2 : nullptr,
                      (status && op == Op::ENCAPS) ? (int32_t*)(d + o_st) : nullptr, st);
+  HT(5);
   ctx->flag_next = false;
-  ctx->hin_next[0] = ctx->hin_next[1] = nullptr;
+  ctx->hin_next = nullptr;
   hipError_t e = hipSuccess;
   if (!rc && spin) {
     // bounded spin; a kernel that never stores the ticket (a launch or execution error) falls
@@ -512,6 +531,7 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
       }
       if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
     }
+    HT(6);
     if (!seen) e = hipStreamSynchronize(st);
   } else if (!rc) {
     e = hipStreamSynchronize(st);
@@ -524,6 +544,7 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   }
   if (rc) (void)hipStreamSynchronize(st);  // nothing may still read or write the mirror
   OQS_MEM_cleanse(h, total);  // coins, secret keys and shared secrets do not outlive the call
+  HT(7);
   return rc;
 }
 
@@ -612,10 +633,13 @@ static qrk_ctx* default_ctx() {
 }
 
 static OQS_STATUS single(const AlgInfo& a, Op op, uint8_t* o1, uint8_t* o2, const uint8_t* i1, const uint8_t* i2) {
+  HT(0);
   qrk_ctx* ctx = default_ctx();
   std::lock_guard<std::mutex> lk(ctx->mu);
   int32_t status = 0;
+  HT(1);
   int rc = run_batch_host(ctx, a, op, 1, o1, o2, i1, i2, op == Op::KEYPAIR ? nullptr : &status);
+  HT(9);
   // ML-KEM encaps: the FIPS 203 modulus check; HQC decaps: liboqs returns OQS_ERROR when the
   // re-encryption check fails (the shared secret K(sigma || ct) is still written)
   if (rc == 0 && status != 0)

@@ -1372,10 +1372,14 @@ __device__ __forceinline__ void wave_phase() {
 // SampleNTT entry e = x K + y (FIPS 203 Alg. 7) on one wave: SHAKE128(rho || x || y) squeezed
 // block by block; each block's 56 byte triples are parsed by lanes 0-55 (two candidates each)
 // and the accepted ones placed by ballot prefix counts, so the wave keeps FIPS order:
-// place(j, value) for coefficient j.  pbuf: this wave's 44-dword LDS parse buffer.
-template <int K, typename Place>
+// place(j, value) for coefficient j.  pbuf: this wave's 44-dword LDS parse buffer.  after_block(cnt):
+// called with the running count of accepted values once a block's values are placed.
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <int K, typename Place, typename Hook = NoHook>
 __device__ __forceinline__ void xof_coop_place(const uint64_t* __restrict__ rho, int e, uint32_t* __restrict__ pbuf,
-                                               const Coop& c, Place place) {
+                                               const Coop& c, Place place, Hook after_block = Hook()) {
   const int i = c.idx, lane = threadIdx.x & 63;
   CState s;
   if (i >= 0 && i < 4) cs_xor(s, rho[i]);
@@ -1406,6 +1410,7 @@ __device__ __forceinline__ void xof_coop_place(const uint64_t* __restrict__ rho,
     if (a2 && p2 < 256) place(p2, d2);
     cnt += __popcll(m1) + __popcll(m2);
     wave_phase();  // this block's parse reads are done before the next block's pbuf writes
+    after_block(cnt);
   }
 }
 // ... into the single-shot layout: coefficient j of entry e at int16 index ((j / 8) 16 + e) 8 + j % 8
@@ -1610,9 +1615,13 @@ __device__ __forceinline__ bool enc_v_one(const OneLds& sl, const uint8_t* __res
   return group_or(bad ? 1u : 0u) != 0;
 }
 
+// The public input of a single-shot host call (n == 1) passed by value, so the kernel does not read
+// it over PCIe before H(ek); the secret inputs (the coins m here, dk for Decaps, d || z for KeyGen)
+// stay in the pinned mirror, which the host wipes after the call: the HIP runtime's kernel-argument
+// pool is never wiped.
 template <int K>
-struct EncIn {  // one handshake's Encaps inputs passed by value (single-shot host calls)
-  uint64_t pk[P<K>::PK / 8], coins[4];
+struct EncIn {
+  uint64_t pk[P<K>::PK / 8];
 };
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const uint8_t* __restrict__ pk,
@@ -1628,9 +1637,9 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   constexpr int EKW = P<K>::PK / 8;
   SS_MARK(threadIdx.x == 0, 0);
   SS_CLK(threadIdx.x == 0, 20);
-  // inputs from memory, or (pk == nullptr: n == 1 host calls) from the kernel argument
+  // ek from memory, or (pk == nullptr: n == 1 host calls) from the kernel argument; m from memory
   stage_in(sl.io, pk ? (const uint64_t*)(pk + hs * P<K>::PK) : in.pk, EKW);
-  stage_in(sl.io + EKW, pk ? (const uint64_t*)(coins + hs * 32) : in.coins, 4);
+  stage_in(sl.io + EKW, (const uint64_t*)(coins + hs * 32), 4);
   __syncthreads();
   const uint64_t* ek = sl.io;
   if (wave == 0) {  // (K, r) = G(m || H(ek)): the critical chain
@@ -1675,16 +1684,10 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_encaps_one(size_t n, const u
   wipe_one(sl, done, ticket);
 }
 
-// one handshake's Decaps inputs passed by value (single-shot host calls): up to ML-KEM-1024's 4736 B,
-// past the 4 KB of kernel arguments often quoted -- a 4800-byte argument launches and reads back
-// correctly on this stack (tools/kernarg_probe.hip, profiles/r4/single_shot/kernarg_probe_4800B.txt)
-template <int K, bool FITS = (P<K>::CT + P<K>::SK <= 4736)>
-struct DecIn {
-  uint64_t ct[P<K>::CT / 8], sk[P<K>::SK / 8];
-};
+// the ciphertext of a single-shot host call passed by value (<= 1568 B); dk stays in the pinned mirror
 template <int K>
-struct DecIn<K, false> {
-  uint64_t ct[1], sk[1];
+struct DecIn {
+  uint64_t ct[P<K>::CT / 8];
 };
 template <int K>
 __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const uint8_t* __restrict__ ct,
@@ -1697,9 +1700,9 @@ __global__ __launch_bounds__(64 * ONE_WAVES) void k_decaps_one(size_t n, const u
   const Coop c = coop_init();
   const int i = c.idx;
   constexpr int CTW = P<K>::CT / 8, SKW = P<K>::SK / 8;
-  // inputs from memory, or (ct == nullptr: n == 1 host calls) from the kernel argument
+  // c from memory, or (ct == nullptr: n == 1 host calls) from the kernel argument; dk from memory
   stage_in(sl.io, ct ? (const uint64_t*)(ct + hs * P<K>::CT) : in.ct, CTW);
-  stage_in(sl.io + CTW, ct ? (const uint64_t*)(sk + hs * P<K>::SK) : in.sk, SKW);
+  stage_in(sl.io + CTW, (const uint64_t*)(sk + hs * P<K>::SK), SKW);
   uint8_t* cc = (uint8_t*)sl.io;                   // the received ciphertext (LDS copy)
   const uint8_t* dk = (const uint8_t*)(sl.io + CTW);  // dk (LDS copy)
   constexpr int XW = ONE_WAVES - 3;  // SampleNTT waves 2 .. ONE_WAVES - 2; the last wave computes v
@@ -1866,6 +1869,10 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
 #ifndef QRK_KG_MULTI_MAX
 #define QRK_KG_MULTI_MAX 16
 #endif
+// 1: k_keygen_pipe (H(ek) pipelined with SampleNTT, below); 0: k_keygen_multi
+#ifndef QRK_KG_PIPE
+#define QRK_KG_PIPE 1
+#endif
 struct MkScr {
   uint4 xs[32 * 16];        // SampleNTT entries, load_sampled<16> layout (K^2 <= 16)
   uint32_t bop[4][16][16];  // NTT(s_j) basemul operands, word w of lane L at [j][w][L]
@@ -2020,6 +2027,363 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
     // n == 1: the only handshake; the flag means every output is visible to the host
     __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// ------------------------------------------------------------ single-shot KeyGen, H(ek) pipelined
+// k_keygen_multi's critical path is G, three SampleNTT blocks, the count-in, t_hat, then the nine
+// permutations of H(ek) = SHA3-256(t_hat || rho): 13 sequential cooperative permutations.  H(ek)
+// absorbs t_hat_0 first, and t_hat_0's coefficient c needs only coefficient c of the row-0 entries
+// A[0][j], which SampleNTT emits in FIPS order: so H's first blocks can run while SampleNTT still
+// squeezes.  k_keygen_pipe, per handshake, 3K workgroups of K + 2 waves:
+//   PRF items (2K, one wave busy): G, PRF(sigma, N), CBD, NTT -> NTT(s_j) basemul operands or
+//     NTT(e_i) into the scratch, published to the others (write-through sc1 stores, a drained wave,
+//     then an sc1 flag store: MI355X_MICROARCH.md "Valid forms", table row 1); dk's s_hat bytes
+//   row r = 1 .. K-1 (K waves): G and SampleNTT A[r][j] (wave j), then t_hat_r, published the same
+//     way; ek / dk's t_hat_r bytes
+//   row 0 = the collector (K + 2 waves): waves 0 .. K-1 G and SampleNTT A[0][j], bumping an LDS count
+//     after every block; wave K computes t_hat_0 in three ranges of coefficient pairs as soon as
+//     every A[0][j] has emitted them (H(ek) blocks 0, 1 and 2 need t_hat_0 bytes < 136, < 272, all),
+//     then copies t_hat_1 .. t_hat_{K-1} in from the row workgroups; wave K + 1 computes G itself
+//     and absorbs ek block by block as its bytes arrive
+// The critical path becomes G, SampleNTT's first two blocks (one block yields ~91 coefficients,
+// H's block 0 needs 92), then the nine H(ek) permutations: 11 permutations.  Every consumer polls
+// one flag word with relaxed sc1 loads (bounded spin) and loads the payload with sc1 loads only.
+// The collector waits until every other workgroup has published its host outputs (system-scope
+// release before the flag when the outputs are host memory), wipes the secret scratch (s_hat,
+// e_hat), resets the flags and stores the completion ticket.
+struct PipeScr {
+  uint32_t bop[4][16][16];  // NTT(s_j) basemul operands, word w of lane L at [j][w][L] (secret)
+  float ef[4][16][16];      // NTT(e_i), coefficient t of lane L at [i][t][L] (secret)
+  uint32_t th[4][96];       // t_hat_r as ek bytes, rows 1 .. K-1 (public)
+};
+// flag words per handshake (ctx->kg_cnt, zeroed at allocation, reset by the collector):
+// [N] PRF item N published, [8 + r] t_hat_r published, [16 + w] workgroup w's outputs written
+constexpr int KG_FLAGS = 32;
+struct PipeLds {
+  uint4 xs[32 * 4];        // the workgroup's K <= 4 entries, load_sampled<4> layout
+  uint32_t pbuf[4][44];    // SampleNTT parse buffers
+  uint32_t bop[4][16][16];  // collector: the NTT(s_j) operands
+  float ef[16][16];        // collector: NTT(e_0)
+  uint64_t io[200];        // collector: ek (1568 B at K = 4)
+  uint64_t rho[4][4];      // per SampleNTT wave
+  uint64_t ps[PRF_W * 16];  // PRF items
+  uint64_t sigma[4];
+  GroupLds g;
+  int prog[4], io_ready;
+};
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// bounded spins (50 ms of the 100 MHz wall clock): a lost hand-off ends the kernel with wrong
+// outputs instead of hanging the GPU
+constexpr uint64_t KG_SPIN_TICKS = 5000000;
+// one wave polls flag words (relaxed sc1 loads, all of them issued per pass); its payload loads
+// after this are sc1 loads only
+template <int NF>
+__device__ __forceinline__ void kg_wait_flags(const uint32_t* const (&f)[NF]) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < KG_SPIN_TICKS) {
+    uint32_t v[NF];
+#pragma unroll
+    for (int k = 0; k < NF; ++k) v[k] = ld_sc1(f[k]);
+    bool all = true;
+#pragma unroll
+    for (int k = 0; k < NF; ++k) all = all && v[k] != 0u;
+    if (all) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+}
+__device__ __forceinline__ void kg_wait_flag(const uint32_t* f) {
+  const uint32_t* const a[1] = {f};
+  kg_wait_flags<1>(a);
+}
+// the storing wave's sc1 stores drained, then one lane stores the flag
+__device__ __forceinline__ void kg_publish(uint32_t* f) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) st_sc1(f, 1u);
+}
+__device__ __forceinline__ void lds_wait_ge(const int* p, int v) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v && wall_clock64() - t0 < KG_SPIN_TICKS)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void lds_release_store(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// (rho, sigma) = G(d || k) on one wave
+__device__ __forceinline__ CState g_keygen_coop(const uint64_t* d, int K, const Coop& c) {
+  const int i = c.idx;
+  CState g;
+  if (i >= 0 && i < 4) cs_xor(g, d[i]);
+  if (i == 4) g.lo ^= (uint32_t)K | (DS_SHA3 << 8);
+  if (i == RW_SHA3_512 - 1) g.hi ^= 0x80000000u;
+  return kf_coop(g, c);
+}
+// SampleNTT A[r][j] = SampleNTT(rho || j || r) on wave j into slot j of the workgroup's entries
+template <int K>
+__device__ __forceinline__ void kg_pipe_sample(PipeLds& sl, const uint64_t* d, int r, int j, const Coop& c) {
+  const CState g = g_keygen_coop(d, K, c);
+  if (c.idx >= 0 && c.idx < 4 && coop_canon(c)) sl.rho[j][c.idx] = cs_word(g);
+  wave_phase();
+  uint16_t* xs16 = (uint16_t*)sl.xs;
+  xof_coop_place<K>(
+      sl.rho[j], j * K + r, sl.pbuf[j], c, [&](int q, uint32_t v) { xs16[(((q >> 3) * 4 + j) << 3) + (q & 7)] = (uint16_t)v; },
+      [&](int cnt) {
+        lds_release_store(&sl.prog[j], cnt < 256 ? cnt : 256);
+        SS_MARK(r == 0 && j == 0 && (threadIdx.x & 63) == 0, cnt < 120 ? 10 : cnt < 210 ? 11 : 12);
+      });
+}
+// The s_hat operands and e_hat_r from the PRF workgroups into LDS (one wave): it waits for their K + 1
+// flags, then issues every 8-byte sc1 load before the first LDS store (one round trip, not one per load)
+template <int K>
+__device__ __forceinline__ void kg_load_ops(PipeLds& sl, const PipeScr& scr, const uint32_t* fl, int r) {
+  const uint32_t* f[K + 1];
+#pragma unroll
+  for (int j = 0; j < K; ++j) f[j] = &fl[j];
+  f[K] = &fl[K + r];
+  kg_wait_flags<K + 1>(f);
+  const int lane = threadIdx.x & 63;
+  constexpr int NB = K * 128 / 64, NE = 128 / 64;  // u64 words per lane
+  uint64_t vb[NB], ve[NE];
+  const uint64_t* sb = (const uint64_t*)&scr.bop[0][0][0];
+  const uint64_t* se = (const uint64_t*)&scr.ef[r][0][0];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) vb[k] = __hip_atomic_load((const gu64*)(sb + lane + 64 * k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < NE; ++k) ve[k] = __hip_atomic_load((const gu64*)(se + lane + 64 * k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) ((uint64_t*)&sl.bop[0][0][0])[lane + 64 * k] = vb[k];
+#pragma unroll
+  for (int k = 0; k < NE; ++k) ((uint64_t*)&sl.ef[0][0])[lane + 64 * k] = ve[k];
+  wave_phase();
+}
+// t_hat_r coefficient pair p (K-term basemul from the entries in LDS and the s_hat operands, + e_hat)
+// as its three ek bytes
+template <int K, typename BopAt, typename EfAt>
+__device__ __forceinline__ uint32_t kg_pipe_pair(const PipeLds& sl, int p, BopAt bop_at, EfAt ef_at) {
+  const int L = p >> 3, u = p & 7;
+  int a0 = 0, a1 = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t a = ((const uint32_t*)sl.xs)[(((2 * p) >> 3) * 4 + j) * 4 + (p & 3)];
+    a0 = dot2(a, bop_at(j, u, L), a0);
+    a1 = dot2(a, bop_at(j, 8 + u, L), a1);
+  }
+  const uint32_t t0 = (uint32_t)canon_f(acc_to_f(a0) + ef_at(2 * u, L));
+  const uint32_t t1 = (uint32_t)canon_f(acc_to_f(a1) + ef_at(2 * u + 1, L));
+  return t0 | (t1 << 12);  // 24 bits, little-endian ek bytes 3p .. 3p + 2
+}
+template <int K>
+__global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const uint8_t* __restrict__ coins,
+                                                              uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
+                                                              PipeScr* __restrict__ scr_all, uint32_t* __restrict__ flags,
+                                                              uint32_t* done, uint32_t ticket) {
+  constexpr int NWG = 3 * K, PKB = P<K>::PK;
+  __shared__ __attribute__((aligned(16))) PipeLds sl;
+  const size_t hs = blockIdx.x / NWG;
+  const int role = (int)(blockIdx.x % NWG);  // [0, 2K) PRF items, [2K, 3K - 1) rows 1 .. K-1, 3K - 1 the collector
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const Coop c = coop_init();
+  const int i = c.idx;
+  PipeScr& scr = scr_all[hs];
+  uint32_t* fl = flags + hs * KG_FLAGS;
+  uint8_t* ek = pk + hs * PKB;
+  uint8_t* dk = sk + hs * P<K>::SK;
+  const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+  auto wipe_lds = [&] {
+    __syncthreads();
+    uint4* w = (uint4*)&sl;
+    for (int x = threadIdx.x; x < (int)(sizeof(PipeLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
+  };
+  // a non-collector workgroup's last act: its host-memory outputs released at system scope, then
+  // its flag (the collector's done ticket follows every such flag)
+  auto outputs_done = [&](int w) {
+    if (done) __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_sc1(&fl[16 + w], 1u);
+    }
+  };
+  if (threadIdx.x < 4) sl.prog[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sl.io_ready = 0;
+  __syncthreads();
+  SS_MARK(role == NWG - 1 && threadIdx.x == 0, 0);
+  if (role < 2 * K) {  // ------------------------------------------------ PRF item N = role
+    const int N = role;
+    if (wave == 0) {
+      const CState g = g_keygen_coop(d, K, c);
+      if (i >= 4 && i < 8 && coop_canon(c)) sl.sigma[i - 4] = cs_word(g);
+      wave_phase();
+      prf_coop<P<K>::ETA1>(sl.sigma, N, sl.ps, c);
+      wave_phase();
+      PF16 f;
+      if (lane < 16) {
+        cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1, 16>(sl.ps, (size_t)N, lane));
+        contig_to_stride_f(f, (float*)sl.g.poly, lane);
+        ntt_fwd_f<false>(f, (float*)sl.g.poly, lane);
+        if (N < K) {
+          const BOp b = make_bop_f(f, lane);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            st_sc1(&scr.bop[N][u][lane], b.b0[u]);
+            st_sc1(&scr.bop[N][8 + u][lane], b.b1[u]);
+          }
+        } else {
+#pragma unroll
+          for (int x = 0; x < 16; ++x) st_sc1((uint32_t*)&scr.ef[N - K][x][lane], __float_as_uint(f.v[x]));
+        }
+      }
+      kg_publish(&fl[N]);
+      SS_MARK(N == 0 && lane == 0, 1);
+      if (N < K && lane < 16) {
+        P16 t;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) t.v[x] = canon_f(f.v[x]);
+        encode12(t, dk + 384 * N, lane);
+      }
+    }
+    outputs_done(N);
+    wipe_lds();
+    return;
+  }
+  const int r = role < NWG - 1 ? role - 2 * K + 1 : 0;  // the matrix row of this workgroup
+  if (wave < K) {  // ------------------------------------------------------ SampleNTT A[r][wave]
+    kg_pipe_sample<K>(sl, d, r, wave, c);
+    SS_MARK(r == 0 && wave == 0 && lane == 0, 2);
+  }
+  if (r > 0) {  // ---------------------------------------------------------- row r's t_hat
+    if (wave == 0) {
+      kg_load_ops<K>(sl, scr, fl, r);
+#pragma unroll
+      for (int j = 0; j < K; ++j) lds_wait_ge(&sl.prog[j], 256);
+      // lane l: pairs l and l + 64
+      uint32_t tb[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = lane + 64 * h;
+        tb[h] = kg_pipe_pair<K>(
+            sl, p, [&](int j, int w, int L) { return sl.bop[j][w][L]; }, [&](int t, int L) { return sl.ef[t][L]; });
+      }
+      uint8_t* io8 = (uint8_t*)sl.io;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = lane + 64 * h;
+        io8[3 * p] = (uint8_t)tb[h];
+        io8[3 * p + 1] = (uint8_t)(tb[h] >> 8);
+        io8[3 * p + 2] = (uint8_t)(tb[h] >> 16);
+      }
+      wave_phase();
+      const uint32_t* io32 = (const uint32_t*)sl.io;
+      for (int w = lane; w < 96; w += 64) st_sc1(&scr.th[r][w], io32[w]);
+      kg_publish(&fl[8 + r]);
+      SS_MARK(r == 1 && lane == 0, 19);
+      for (int w = lane; w < 96; w += 64) {
+        ((uint32_t*)(ek + 384 * r))[w] = io32[w];
+        ((uint32_t*)(dk + 384 * K + 384 * r))[w] = io32[w];
+      }
+    }
+    outputs_done(2 * K + r - 1);
+    wipe_lds();
+    return;
+  }
+  // ------------------------------------------------------------------------ the collector (row 0)
+  uint8_t* io8 = (uint8_t*)sl.io;
+  if (wave == K) {  // t_hat_0 pairs as A[0][j] fills, then the other rows' t_hat
+    kg_load_ops<K>(sl, scr, fl, 0);
+    SS_MARK(lane == 0, 22);
+    // pair ranges whose bytes complete H(ek) blocks 0, 1, 2: pair p is ek bytes 3p .. 3p + 2
+    constexpr int LIM[4] = {0, 46, 91, 128};
+#pragma unroll 1
+    for (int b = 0; b < 3; ++b) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) lds_wait_ge(&sl.prog[j], 2 * LIM[b + 1]);
+      const int p = LIM[b] + lane;
+      if (p < LIM[b + 1]) {
+        const uint32_t t = kg_pipe_pair<K>(
+            sl, p, [&](int j, int w, int L) { return sl.bop[j][w][L]; }, [&](int t, int L) { return sl.ef[t][L]; });
+        io8[3 * p] = (uint8_t)t;
+        io8[3 * p + 1] = (uint8_t)(t >> 8);
+        io8[3 * p + 2] = (uint8_t)(t >> 16);
+      }
+      lds_release_store(&sl.io_ready, 3 * LIM[b + 1]);
+    }
+    SS_MARK(lane == 0, 3);
+    const uint32_t* io32 = (const uint32_t*)sl.io;
+    for (int w = lane; w < 96; w += 64) {
+      ((uint32_t*)ek)[w] = io32[w];
+      ((uint32_t*)(dk + 384 * K))[w] = io32[w];
+    }
+    for (int rr = 1; rr < K; ++rr) {
+      kg_wait_flag(&fl[8 + rr]);
+      const uint64_t* st = (const uint64_t*)&scr.th[rr][0];
+      uint64_t v = 0;
+      if (lane < 48) v = __hip_atomic_load((const gu64*)(st + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < 48) sl.io[48 * rr + lane] = v;
+      lds_release_store(&sl.io_ready, 384 * (rr + 1));
+    }
+    SS_MARK(lane == 0, 5);
+  } else if (wave == K + 1) {  // H(ek), block by block as ek's bytes arrive
+    __builtin_amdgcn_s_setprio(3);
+    const uint64_t zw = (i >= 0 && i < 4) ? d[4 + i] : 0;
+    const CState g = g_keygen_coop(d, K, c);
+    if (i >= 0 && i < 4 && coop_canon(c)) {
+      sl.io[48 * K + i] = cs_word(g);
+      ((uint64_t*)(ek + 384 * K))[i] = cs_word(g);
+      ((uint64_t*)(dk + 768 * K))[i] = cs_word(g);
+    }
+    wave_phase();
+    SS_MARK(lane == 0, 7);
+    constexpr int RW = RW_SHA3_256, NW = PKB / 8, NFULL = NW / RW, TAIL = NW % RW;
+    const bool rl = i >= 0 && i < RW;
+    CState s;
+#pragma unroll 1
+    for (int b = 0; b < NFULL; ++b) {
+      const int need = 8 * RW * (b + 1) < 384 * K ? 8 * RW * (b + 1) : 384 * K;
+      lds_wait_ge(&sl.io_ready, need);
+      SS_MARK(lane == 0 && b < 4, 8 + (b == 0 ? 0 : b == 1 ? 5 : b == 2 ? 1 : 6));
+      if (rl) cs_xor(s, sl.io[b * RW + i]);
+      s = kf_coop(s, c);
+    }
+    lds_wait_ge(&sl.io_ready, 384 * K);
+    if (rl && i < TAIL) cs_xor(s, sl.io[NFULL * RW + i]);
+    if (i == TAIL) s.lo ^= DS_SHA3;
+    if (i == RW - 1) s.hi ^= 0x80000000u;
+    s = kf_coop(s, c);
+    if (i >= 0 && i < 4 && coop_canon(c)) {
+      uint64_t* tail = (uint64_t*)(dk + 768 * K + 32);
+      tail[i] = cs_word(s);
+      tail[4 + i] = zw;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    SS_MARK(lane == 0, 4);
+  }
+  // every other workgroup's outputs (and its last scratch / flag access) done, then the secret
+  // scratch wiped, the flags reset and the completion ticket stored
+  if (done) __threadfence_system();
+  __syncthreads();
+  if (wave == 0) {
+    const uint32_t* of[NWG - 1];
+#pragma unroll
+    for (int w = 0; w < NWG - 1; ++w) of[w] = &fl[16 + w];
+    kg_wait_flags<NWG - 1>(of);
+    uint4* sw = (uint4*)&scr;
+    for (int x = lane; x < (int)(offsetof(PipeScr, th) / 16); x += 64) sw[x] = make_uint4(0, 0, 0, 0);
+    if (lane < KG_FLAGS) st_sc1(&fl[lane], 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (done && lane == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    SS_MARK(lane == 0, 6);
+  }
+  wipe_lds();
 }
 
 // ============================================================ multi-role launches
@@ -2255,15 +2619,14 @@ template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
-    KgCoins cv{};
-    const bool by_value = n == 1 && s.host_in1;
-    if (by_value) memcpy(cv.w, s.host_in1, sizeof(cv.w));
+  if (QRK_KG_PIPE && n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
+    QRK_LAUNCH("k_keygen_pipe", s.main, k_keygen_pipe<K>, dim3((unsigned)(n * 3 * K)), dim3(64 * (K + 2)), 0, s.main, n,
+               coins, pk, sk, (PipeScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
+    return hipGetLastError();
+  }
+  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {  // QRK_KG_PIPE=0 builds (A/B): the round-4 kernel
     QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
-               s.main, n, by_value ? nullptr : coins, cv, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr,
-               s.ticket);
-    volatile uint64_t* vw = cv.w;  // the host copy of the coins does not outlive the launch call
-    for (int w = 0; w < 8; ++w) vw[w] = 0;
+               s.main, n, coins, KgCoins{}, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
   if (n <= QRK_SMALL_MAX) {
@@ -2292,15 +2655,10 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
     EncIn<K> in{};
-    const bool by_value = n == 1 && s.host_in1 && s.host_in2;
-    if (by_value) {
-      memcpy(in.pk, s.host_in1, sizeof(in.pk));
-      memcpy(in.coins, s.host_in2, sizeof(in.coins));
-    }
+    const bool by_value = n == 1 && s.host_in1;
+    if (by_value) memcpy(in.pk, s.host_in1, sizeof(in.pk));
     QRK_LAUNCH("k_encaps_one", s.main, k_encaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n,
                by_value ? nullptr : pk, coins, in, ct, ss, status, n == 1 ? s.done : nullptr, s.ticket);
-    volatile uint64_t* vc = in.coins;  // the host copy of the coins does not outlive the launch call
-    for (int w = 0; w < 4; ++w) vc[w] = 0;
     return hipGetLastError();
   }
   hipStream_t st = s.main;
@@ -2325,18 +2683,10 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   ScratchView v = carve(scratch, K, C);
   if (n <= QRK_SMALL_MAX) {
     DecIn<K> in{};
-    constexpr bool FITS = sizeof(in.ct) == P<K>::CT;
-    const bool by_value = FITS && n == 1 && s.host_in1 && s.host_in2;
-    if constexpr (FITS) {
-      if (by_value) {
-        memcpy(in.ct, s.host_in1, sizeof(in.ct));
-        memcpy(in.sk, s.host_in2, sizeof(in.sk));
-      }
-    }
+    const bool by_value = n == 1 && s.host_in1;
+    if (by_value) memcpy(in.ct, s.host_in1, sizeof(in.ct));
     QRK_LAUNCH("k_decaps_one", s.main, k_decaps_one<K>, dim3((unsigned)n), dim3(64 * ONE_WAVES), 0, s.main, n,
                by_value ? nullptr : ct, sk, in, ss, n == 1 ? s.done : nullptr, s.ticket);
-    volatile uint64_t* vs = in.sk;  // the host copy of the secret key does not outlive the launch call
-    for (size_t w = 0; w < sizeof(in.sk) / 8; ++w) vs[w] = 0;
     return hipGetLastError();
   }
   hipStream_t st = s.main;
@@ -2363,8 +2713,10 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
   // the multi-workgroup KeyGen (n <= QRK_KG_MULTI_MAX) keeps one MkScr (16 KiB) per handshake in
   // the scratch; every other path needs scratch_words (about 5.1 KB per ML-KEM-768 handshake)
   const size_t C = mlkem::round64(chunk);
-  return std::max(mlkem::scratch_words(a.k, C) * 8, std::min(C, (size_t)QRK_KG_MULTI_MAX) * sizeof(mlkem::MkScr));
+  return std::max(mlkem::scratch_words(a.k, C) * 8,
+                  std::min(C, (size_t)QRK_KG_MULTI_MAX) * std::max(sizeof(mlkem::MkScr), sizeof(mlkem::PipeScr)));
 }
+size_t mlkem_kg_flag_words() { return (size_t)QRK_KG_MULTI_MAX * mlkem::KG_FLAGS; }
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }

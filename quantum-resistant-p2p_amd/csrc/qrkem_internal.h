@@ -76,6 +76,8 @@ void mlkem_records_span(const AlgInfo& a, size_t C, size_t* off, size_t* bytes);
 size_t mlkem_small_max();
 // ML-KEM KeyGen batches up to this size run one workgroup per SampleNTT / PRF item (latency)
 size_t mlkem_kg_multi_max();
+// flag / counter words of the single-shot multi-workgroup KeyGen (ctx->kg_cnt)
+size_t mlkem_kg_flag_words();
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 
@@ -93,10 +95,10 @@ struct Streams {
   // per-handshake arrival counters of the multi-workgroup single-shot ML-KEM KeyGen (device,
   // QRK_KG_MULTI_MAX words, zero between calls: the last workgroup of a handshake resets its word)
   uint32_t* kg_cnt = nullptr;
-  // single-shot ML-KEM (n == 1, host-pointer call): the inputs in host memory (KeyGen: coins;
-  // Encaps: pk, coins); the kernel takes them as a kernel argument instead of reading them over PCIe
+  // single-shot ML-KEM (n == 1, host-pointer call): the public input in host memory (Encaps: pk;
+  // Decaps: c), passed as a kernel argument instead of read over PCIe.  Secret inputs are never
+  // passed by value: the runtime's kernel-argument pool is not wiped.
   const uint8_t* host_in1 = nullptr;
-  const uint8_t* host_in2 = nullptr;
 };
 
 // All pointers are device pointers; n handshakes processed as one chunk

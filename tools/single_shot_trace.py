@@ -19,9 +19,12 @@ fn = LIB.qrk_dbg_ss_trace
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 MARKS = {
     # k_keygen_multi (n = 1): one workgroup per PRF / SampleNTT item, the last to count in finishes
-    "keypair": {14: "last item workgroup started", 13: "G(d||k) done (workgroup 0)",
-                15: "first SampleNTT item done", 4: "last workgroup counted in", 16: "t rows done",
-                17: "H(ek) done", 18: "wipes + system fence done (flag next)"},
+    # k_keygen_pipe (n = 1, the default): t = 0 is the collector workgroup's start
+    "keypair": {1: "PRF item 0 published", 7: "H wave: G done", 10: "SampleNTT A[0][0] block 1",
+                11: "block 2", 12: "block 3", 2: "A[0][0] done", 22: "t wave: s_hat, e_hat loaded",
+                8: "H block 0 starts", 13: "H block 1 starts", 9: "H block 2 starts", 14: "H block 3 starts",
+                3: "t_hat_0 done", 19: "row 1 t_hat published", 5: "t_hat_1.. copied in", 4: "H(ek) done",
+                6: "done (wipe, flags reset)"},
     "encaps": {1: "H(ek)+G done", 3: "wave 1 SampleNTT done", 2: "wave 0 PRF + NTT(y_0) done", 4: "sync", 7: "u rows done"},
     "decaps": {8: "decrypt done", 9: "G done", 12: "wave 2 SampleNTT done", 10: "wave 2 PRF done", 4: "rows start",
                11: "J done", 6: "rows done, v + Kbar ready", 7: "select done"},
