@@ -2376,6 +2376,8 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
 #pragma unroll
     for (int w = 0; w < NWG - 1; ++w) of[w] = &fl[16 + w];
     kg_wait_flags<NWG - 1>(of);
+    // key hygiene order: the secret scratch (s_hat, e_hat) is wiped and the flags reset, the stores
+    // drained, and only then is the completion ticket stored for the host
     uint4* sw = (uint4*)&scr;
     for (int x = lane; x < (int)(offsetof(PipeScr, th) / 16); x += 64) sw[x] = make_uint4(0, 0, 0, 0);
     if (lane < KG_FLAGS) st_sc1(&fl[lane], 0u);
