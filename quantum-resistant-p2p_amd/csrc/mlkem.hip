@@ -2204,8 +2204,8 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
     uint4* w = (uint4*)&sl;
     for (int x = threadIdx.x; x < (int)(sizeof(PipeLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
   };
-  // a non-collector workgroup's last act: its host-memory outputs released at system scope, then
-  // its flag (the collector's done ticket follows every such flag)
+  // a non-collector workgroup's last act (after its LDS wipe): its host-memory outputs released at
+  // system scope, then its flag (the collector's done ticket follows every such flag)
   auto outputs_done = [&](int w) {
     if (done) __threadfence_system();
     __syncthreads();
@@ -2252,8 +2252,8 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         encode12(t, dk + 384 * N, lane);
       }
     }
+    wipe_lds();  // sigma, the PRF output and NTT(s) / NTT(e): wiped before the flag that ends this workgroup
     outputs_done(N);
-    wipe_lds();
     return;
   }
   const int r = role < NWG - 1 ? role - 2 * K + 1 : 0;  // the matrix row of this workgroup
@@ -2292,8 +2292,8 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         ((uint32_t*)(dk + 384 * K + 384 * r))[w] = io32[w];
       }
     }
+    wipe_lds();  // the s_hat / e_hat copies: wiped before the flag that ends this workgroup
     outputs_done(2 * K + r - 1);
-    wipe_lds();
     return;
   }
   // ------------------------------------------------------------------------ the collector (row 0)
@@ -2335,13 +2335,6 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
   } else if (wave == K + 1) {  // H(ek), block by block as ek's bytes arrive
     __builtin_amdgcn_s_setprio(3);
     const uint64_t zw = (i >= 0 && i < 4) ? d[4 + i] : 0;
-    const CState g = g_keygen_coop(d, K, c);
-    if (i >= 0 && i < 4 && coop_canon(c)) {
-      sl.io[48 * K + i] = cs_word(g);
-      ((uint64_t*)(ek + 384 * K))[i] = cs_word(g);
-      ((uint64_t*)(dk + 768 * K))[i] = cs_word(g);
-    }
-    wave_phase();
     SS_MARK(lane == 0, 7);
     constexpr int RW = RW_SHA3_256, NW = PKB / 8, NFULL = NW / RW, TAIL = NW % RW;
     const bool rl = i >= 0 && i < RW;
@@ -2354,7 +2347,18 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
       if (rl) cs_xor(s, sl.io[b * RW + i]);
       s = kf_coop(s, c);
     }
+    // rho (ek's last 32 bytes, in the final partial block for every K) from SampleNTT wave 0's copy
+    // of G's output: wave 0 wrote it before its first progress release, which the t_hat wave acquired
+    // before it released io_ready (this wave computes no G of its own: one cooperative permutation
+    // fewer beside the SampleNTT waves)
     lds_wait_ge(&sl.io_ready, 384 * K);
+    if (i >= 0 && i < 4 && coop_canon(c)) {
+      const uint64_t rw = sl.rho[0][i];
+      sl.io[48 * K + i] = rw;
+      ((uint64_t*)(ek + 384 * K))[i] = rw;
+      ((uint64_t*)(dk + 768 * K))[i] = rw;
+    }
+    wave_phase();
     if (rl && i < TAIL) cs_xor(s, sl.io[NFULL * RW + i]);
     if (i == TAIL) s.lo ^= DS_SHA3;
     if (i == RW - 1) s.hi ^= 0x80000000u;
@@ -2367,25 +2371,25 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
     __builtin_amdgcn_s_setprio(0);
     SS_MARK(lane == 0, 4);
   }
-  // every other workgroup's outputs (and its last scratch / flag access) done, then the secret
-  // scratch wiped, the flags reset and the completion ticket stored
+  // Completion, in key-hygiene order: this workgroup's outputs released; its LDS (which holds copies
+  // of s_hat and e_hat_0) wiped; every other workgroup's outputs (and its last scratch / flag
+  // access) done; the secret scratch (s_hat, e_hat) wiped and the flags reset; those stores drained;
+  // and only then the completion ticket stored for the host -- the ticket is the kernel's last act.
   if (done) __threadfence_system();
+  wipe_lds();
   __syncthreads();
   if (wave == 0) {
     const uint32_t* of[NWG - 1];
 #pragma unroll
     for (int w = 0; w < NWG - 1; ++w) of[w] = &fl[16 + w];
     kg_wait_flags<NWG - 1>(of);
-    // key hygiene order: the secret scratch (s_hat, e_hat) is wiped and the flags reset, the stores
-    // drained, and only then is the completion ticket stored for the host
     uint4* sw = (uint4*)&scr;
     for (int x = lane; x < (int)(offsetof(PipeScr, th) / 16); x += 64) sw[x] = make_uint4(0, 0, 0, 0);
     if (lane < KG_FLAGS) st_sc1(&fl[lane], 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (done && lane == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     SS_MARK(lane == 0, 6);
+    if (done && lane == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  wipe_lds();
 }
 
 // ============================================================ multi-role launches
