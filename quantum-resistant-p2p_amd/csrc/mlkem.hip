@@ -31,6 +31,7 @@
 
 #include "keccak.cuh"
 #include "keccak_coop.cuh"
+#include "keccak_pair.cuh"
 #include "qrkem_internal.h"
 
 namespace qrk {
@@ -548,6 +549,63 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
   absorb_words<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE, false>(s, [&](int w) { return w < 4 ? z[w] : c[w - 4]; });
 #pragma unroll
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
+}
+
+// The same three sponges on a lane pair (keccak_pair.cuh: the even lane holds the low halves of the
+// state words, the odd lane the high halves) for chunks of at most QRK_PAIR_FRONT_MAX handshakes:
+// there the fronts' lane-per-handshake waves (one per SIMD at 2^14 handshakes) are the critical path
+// of their launches.  `half` = lane & 1, hm = all-ones on the odd lane.
+template <int K>
+__device__ __forceinline__ void front_encaps_pair(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ coins,
+                                                  size_t hs, int half, uint32_t hm, uint8_t* __restrict__ ss,
+                                                  uint64_t* __restrict__ seeds) {
+  const uint32_t* ek = (const uint32_t*)(pk + hs * P<K>::PK);
+  PState s;
+  pzero(s);
+  pabsorb<RW_SHA3_256, P<K>::PK / 8, DS_SHA3>(s, hm, [&](int w) { return ek[2 * w + half]; });
+  uint32_t h[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) h[w] = s.a[w];
+  const uint32_t* m = (const uint32_t*)(coins + hs * 32);
+  pzero(s);
+  pabsorb<RW_SHA3_512, 8, DS_SHA3>(s, hm, [&](int w) { return w < 4 ? m[2 * w + half] : h[w - 4]; });
+  uint32_t* k_out = (uint32_t*)(ss + hs * 32);
+  uint32_t* r_out = (uint32_t*)(seeds + hs * 4);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    k_out[2 * w + half] = s.a[w];
+    r_out[2 * w + half] = s.a[4 + w];
+  }
+}
+template <int K>
+__device__ __forceinline__ void g_decaps_pair(const uint8_t* __restrict__ sk, const uint64_t* __restrict__ mprime,
+                                              size_t hs, int half, uint32_t hm, uint64_t* __restrict__ seeds,
+                                              uint64_t* __restrict__ kprime) {
+  const uint32_t* h = (const uint32_t*)(sk + hs * P<K>::SK + 768 * K + 32);
+  const uint32_t* m = (const uint32_t*)(mprime + hs * 4);
+  PState s;
+  pzero(s);
+  pabsorb<RW_SHA3_512, 8, DS_SHA3>(s, hm, [&](int w) { return w < 4 ? m[2 * w + half] : h[2 * (w - 4) + half]; });
+  uint32_t* kp = (uint32_t*)(kprime + hs * 4);
+  uint32_t* sd = (uint32_t*)(seeds + hs * 4);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    kp[2 * w + half] = s.a[w];
+    sd[2 * w + half] = s.a[4 + w];
+  }
+}
+template <int K>
+__device__ __forceinline__ void j_decaps_pair(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk, size_t hs,
+                                              int half, uint32_t hm, uint64_t* __restrict__ kbar) {
+  const uint32_t* z = (const uint32_t*)(sk + hs * P<K>::SK + 768 * K + 64);
+  const uint32_t* c = (const uint32_t*)(ct + hs * P<K>::CT);
+  PState s;
+  pzero(s);
+  pabsorb<RW_SHAKE256, 4 + P<K>::CT / 8, DS_SHAKE>(s, hm,
+                                                   [&](int w) { return w < 4 ? z[2 * w + half] : c[2 * (w - 4) + half]; });
+  uint32_t* kb = (uint32_t*)(kbar + hs * 4);
+#pragma unroll
+  for (int w = 0; w < 4; ++w) kb[2 * w + half] = s.a[w];
 }
 
 // ============================================================ 16-lane polynomial groups
@@ -1869,9 +1927,12 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
 #ifndef QRK_KG_MULTI_MAX
 #define QRK_KG_MULTI_MAX 16
 #endif
-// 1: k_keygen_pipe (H(ek) pipelined with SampleNTT, below); 0: k_keygen_multi
+// 1: k_keygen_pipe (H(ek) pipelined with SampleNTT, below; measured 37.5 against 41.6 us per kernel,
+// profiles/r5/single_shot/); 0 (default): k_keygen_multi.  The pipelined kernel stays opt-in
+// (tools/build_variant.sh ... -DQRK_KG_PIPE=1) until its completion / key-wipe ordering has been
+// reviewed.
 #ifndef QRK_KG_PIPE
-#define QRK_KG_PIPE 1
+#define QRK_KG_PIPE 0
 #endif
 struct MkScr {
   uint4 xs[32 * 16];        // SampleNTT entries, load_sampled<16> layout (K^2 <= 16)
@@ -2455,6 +2516,62 @@ struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
     if (hs < n) j_decaps_hs<K>(ct, sk, hs, kbar);
   }
 };
+// lane-pair forms of the three sponge roles (keccak_pair.cuh), 128 handshakes per workgroup
+#ifndef QRK_PAIR_FRONT_MAX
+#define QRK_PAIR_FRONT_MAX (1 << 15)
+#endif
+#ifndef QRK_PAIR_PRIO
+#define QRK_PAIR_PRIO 0
+#endif
+struct PairLane {
+  size_t hs;
+  int half;
+  uint32_t hm;
+};
+__device__ __forceinline__ PairLane pair_lane(unsigned vb) {
+  if (QRK_PAIR_PRIO) __builtin_amdgcn_s_setprio(QRK_PAIR_PRIO);
+  const size_t t = (size_t)vb * 256 + threadIdx.x;
+  const int half = (int)(t & 1);
+  return {t >> 1, half, half ? 0xFFFFFFFFu : 0u};
+}
+template <int K>
+struct RFrontEncPair {
+  static constexpr int LDS = 0, WPE = 1;
+  const uint8_t *pk, *coins;
+  size_t n;
+  uint8_t* ss;
+  uint64_t* seeds;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const PairLane p = pair_lane(vb);
+    if (p.hs < n) front_encaps_pair<K>(pk, coins, p.hs, p.half, p.hm, ss, seeds);
+  }
+};
+template <int K>
+struct RJDecPair {
+  static constexpr int LDS = 0, WPE = 1;
+  const uint8_t *ct, *sk;
+  size_t n;
+  uint64_t* kbar;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const PairLane p = pair_lane(vb);
+    if (p.hs < n) j_decaps_pair<K>(ct, sk, p.hs, p.half, p.hm, kbar);
+  }
+};
+template <int K>
+struct RGDecPair {
+  static constexpr int LDS = 0, WPE = 1;
+  const uint8_t* sk;
+  const uint64_t* mprime;
+  size_t n;
+  uint64_t *seeds, *kprime;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const PairLane p = pair_lane(vb);
+    if (p.hs < n) g_decaps_pair<K>(sk, mprime, p.hs, p.half, p.hm, seeds, kprime);
+  }
+};
 template <int K>
 struct RGDec {  // (K', r') = G(m' || h), lane / handshake
   static constexpr int LDS = 0, WPE = 1;
@@ -2630,7 +2747,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
                coins, pk, sk, (PipeScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
-  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {  // QRK_KG_PIPE=0 builds (A/B): the round-4 kernel
+  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {  // the default (QRK_KG_PIPE=0): the round-4 kernel
     QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
                s.main, n, coins, KgCoins{}, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
@@ -2674,7 +2791,11 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
                          nullptr, (unsigned)((n + GROUPS - 1) / GROUPS)};
-  launch_multi("k_front_encaps+k_xof", {"k_front_encaps", "k_xof"}, s, front, xof_role<K>(rho, n, C, v));
+  if (C <= QRK_PAIR_FRONT_MAX)
+    launch_multi("k_front_encaps+k_xof", {"k_front_encaps", "k_xof"}, s,
+                 RFrontEncPair<K>{pk, coins, n, ss, v.seeds, blocks_for(2 * n)}, xof_role<K>(rho, n, C, v));
+  else
+    launch_multi("k_front_encaps+k_xof", {"k_front_encaps", "k_xof"}, s, front, xof_role<K>(rho, n, C, v));
   launch_fix_prf<K>(rho, n, C, v, prf, s);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
@@ -2705,9 +2826,15 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
-  launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
-               xof_role<K>(rho, n, C, v));
-  launch_one("k_g_decaps", gd, s);
+  if (C <= QRK_PAIR_FRONT_MAX) {
+    launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s,
+                 RJDecPair<K>{ct, sk, n, v.kbar, blocks_for(2 * n)}, dec, xof_role<K>(rho, n, C, v));
+    launch_one("k_g_decaps", RGDecPair<K>{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(2 * n)}, s);
+  } else {
+    launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
+                 xof_role<K>(rho, n, C, v));
+    launch_one("k_g_decaps", gd, s);
+  }
   launch_fix_prf<K>(rho, n, C, v, prf, s);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();

@@ -77,6 +77,33 @@ def test_tampered_implicit_rejection(engines, alg):
 
 
 @pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("n", [(1 << 15) - 5, (1 << 15) + 1])
+def test_pair_front_boundary(engines, alg, n):
+    """Chunks of at most 2^15 handshakes run the sponge fronts (H(ek) + G, J(z || c), G(m' || h))
+    on lane pairs (csrc/keccak_pair.cuh), larger chunks one lane per handshake: both sides of the
+    boundary byte-exact vs the oracle on a sample of indices (both ends included), Decaps with a
+    quarter of the ciphertexts tampered."""
+    import oracle as orc
+    eng = engines[alg]
+    coins = orc.bench_coins(n, 96, seed=4242 + n)
+    kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
+    pk, sk = eng.keypair(coins=_dev(kc))
+    ct, ss = eng.encaps(pk, coins=_dev(ec))
+    bad = _host(ct).copy()
+    flip = (np.arange(n) % 4) == 1
+    bad[flip, 7] ^= 0x20
+    ss2 = _host(eng.decaps(sk, _dev(bad)))
+    pk, sk, ct, ss = map(_host, (pk, sk, ct, ss))
+    idx = np.unique(np.concatenate([np.arange(8), n - 1 - np.arange(8), np.linspace(0, n - 1, 200).astype(int)]))
+    opk, osk = orc.batch_keypair(alg, np.ascontiguousarray(kc[idx]))
+    assert np.array_equal(pk[idx], opk) and np.array_equal(sk[idx], osk)
+    oct_, oss = orc.batch_encaps(alg, opk, np.ascontiguousarray(ec[idx]))
+    assert np.array_equal(ct[idx], oct_) and np.array_equal(ss[idx], oss)
+    assert np.array_equal(ss2[idx], orc.batch_decaps(alg, osk, np.ascontiguousarray(bad[idx])))
+    assert np.array_equal(ss2[~flip], ss[~flip])
+
+
+@pytest.mark.parametrize("alg", ALGS)
 def test_host_pointer_api(engines, alg):
     import oracle as orc
     eng = engines[alg]
