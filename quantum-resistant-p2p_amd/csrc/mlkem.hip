@@ -2523,6 +2523,13 @@ struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
 #ifndef QRK_PAIR_PRIO
 #define QRK_PAIR_PRIO 0
 #endif
+// J(z || c) on lane pairs too: off.  Its launch, {J, decrypt core, SampleNTT}, is throughput-bound at
+// these sizes and the pair form's 1.3x issue slots cost more than its shorter chain saves (2^14:
+// 118.7 against 105.3 us per launch, 45.5e6 against 47.2e6 handshakes/s; the Encaps front + G on
+// pairs alone: +8.8 % at 2^14, +1.5 % at 2^15 against no pairs, profiles/r5/pair_fronts/)
+#ifndef QRK_PAIR_J
+#define QRK_PAIR_J 0
+#endif
 struct PairLane {
   size_t hs;
   int half;
@@ -2827,8 +2834,12 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
   if (C <= QRK_PAIR_FRONT_MAX) {
-    launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s,
-                 RJDecPair<K>{ct, sk, n, v.kbar, blocks_for(2 * n)}, dec, xof_role<K>(rho, n, C, v));
+    if (QRK_PAIR_J)
+      launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s,
+                   RJDecPair<K>{ct, sk, n, v.kbar, blocks_for(2 * n)}, dec, xof_role<K>(rho, n, C, v));
+    else
+      launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
+                   xof_role<K>(rho, n, C, v));
     launch_one("k_g_decaps", RGDecPair<K>{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(2 * n)}, s);
   } else {
     launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
