@@ -9,9 +9,9 @@
 // (theta) + 24 DPP + 24 funnel shifts (rho) + 25 bitop3 (chi) + 2 (iota) = 120 instructions, 29 of
 // them half-rate, against 180 (58 half-rate) for one lane holding the whole state: a chain of sponge
 // permutations finishes ~1.5x sooner on two lanes at 1.3x the issue slots per state.  Used for the
-// ML-KEM batched fronts (H(ek) + G, J(z || c)) at chunks of at most 2^15 handshakes, where one
-// lane-per-handshake wave per SIMD was the critical path of the whole launch (DESIGN.md section 4,
-// round 5).
+// ML-KEM batched Encaps front (H(ek) + G) and Decaps' G(m' || h) at chunks of at most 2^15
+// handshakes, where one lane-per-handshake wave per SIMD was the critical path of the launch
+// (DESIGN.md section 4, round 5).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
