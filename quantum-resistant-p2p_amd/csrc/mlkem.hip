@@ -551,128 +551,6 @@ __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, cons
   for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
 }
 
-// Message staging for the lane-per-handshake sponges that absorb whole records (the Encaps front's
-// H(ek), Decaps' J(z || c)).  Absorbed in place, each lane reads its own record 8 bytes at a time, so
-// one load instruction of a wave touches 64 records 1-1.6 KB apart, and the line a block boundary
-// splits is fetched again for the next block (FETCH_SIZE calibration: 1.55x the record bytes,
-// profiles/r3/fetch_calibration.json).  Staged, the wave reads the next absorb block of its 64 records
-// with consecutive lanes on consecutive words (RW words of one record, then the next record's) into
-// 64 RW words of LDS, and every lane absorbs its own block from there.  src(rec, w): message word w
-// of record rec.  Records >= nrec read nothing (their lanes' results are discarded by the caller).
-#ifndef QRK_FRONT_STAGE
-#define QRK_FRONT_STAGE 1
-#endif
-// Stage words [w0, w0 + NWB) of the wave's 64 records (record r at byte wbase + r * stride) into
-// stage[r * ST + (w - w0) + so]: one coalesced sweep (consecutive lanes, consecutive words), 32-bit
-// offsets from the wave-uniform base, every load issued before the first LDS store.  Records past
-// nrec (from the wave's first) read nothing.
-template <int NWB, int ST>
-__device__ __noinline__ void stage_words(uint64_t* __restrict__ stage, const uint8_t* __restrict__ wbase,
-                                            uint32_t stride, int w0, int so, uint32_t nrec) {
-  const int lane = threadIdx.x & 63;
-  const uint8_t* b0 = wbase + 8 * w0;
-  uint64_t v[NWB];
-#pragma unroll
-  for (int k = 0; k < NWB; ++k) {
-    const uint32_t f = (uint32_t)(lane + 64 * k), r = f / NWB;
-    // record r, word f - r NWB: byte r (stride - 8 NWB) + 8 f past the block's first word
-    v[k] = r < nrec ? *(const uint64_t*)(b0 + r * (stride - 8u * NWB) + 8u * f) : 0;
-  }
-#pragma unroll
-  for (int k = 0; k < NWB; ++k) {
-    const uint32_t f = (uint32_t)(lane + 64 * k);
-    const uint32_t idx = (ST == NWB && so == 0) ? f : f + (f / NWB) * (uint32_t)(ST - NWB) + (uint32_t)so;
-    stage[idx] = v[k];
-  }
-  gsync();  // wave-level release / acquire (the stage is this wave's own)
-}
-// front_encaps_hs / j_decaps_hs with the record absorbs staged (stage: the wave's 64 x 17 words)
-template <int K>
-__device__ __forceinline__ void front_encaps_staged(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ coins,
-                                                    size_t hs, size_t n, uint64_t* __restrict__ stage,
-                                                    uint8_t* __restrict__ ss, uint64_t* __restrict__ seeds) {
-  constexpr int RW = RW_SHA3_256, NW = P<K>::PK / 8, NFULL = NW / RW, TAIL = NW % RW;
-  const int lane = threadIdx.x & 63;
-  // the wave's first record (wave-uniform: its base address lives in SGPRs)
-  const size_t rec0 = ((size_t)__builtin_amdgcn_readfirstlane((uint32_t)(hs >> 32)) << 32) |
-                      __builtin_amdgcn_readfirstlane((uint32_t)(hs - lane));
-  const uint8_t* wbase = pk + rec0 * P<K>::PK;
-  const uint32_t nrec = (uint32_t)(n - rec0 < 64 ? n - rec0 : 64);
-  KState s;
-  kzero(s);
-#pragma unroll 1
-  for (int b = 0; b < NFULL; ++b) {
-    stage_words<RW, RW>(stage, wbase, P<K>::PK, b * RW, 0, nrec);
-#pragma unroll
-    for (int w = 0; w < RW; ++w) kxor(s, w, stage[lane * RW + w]);
-    gsync();  // read before the next block is staged
-    keccak_f(s);
-  }
-  stage_words<TAIL, RW>(stage, wbase, P<K>::PK, NFULL * RW, 0, nrec);
-#pragma unroll
-  for (int w = 0; w < TAIL; ++w) kxor(s, w, stage[lane * RW + w]);
-  s.a[TAIL].lo ^= DS_SHA3;
-  s.a[RW - 1].hi ^= 0x80000000u;
-  keccak_f(s);
-  if (hs >= n) return;
-  uint64_t h[4];
-#pragma unroll
-  for (int w = 0; w < 4; ++w) h[w] = kword(s, w);
-  const uint64_t* m = (const uint64_t*)(coins + hs * 32);
-  kzero(s);
-  absorb_words<RW_SHA3_512, 8, DS_SHA3>(s, [&](int w) { return w < 4 ? m[w] : h[w - 4]; });
-  uint64_t* K_out = (uint64_t*)(ss + hs * 32);
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    K_out[w] = kword(s, w);
-    seeds[hs * 4 + w] = kword(s, 4 + w);
-  }
-}
-// J(z || c): block 0 is z (4 words, read by each lane from its own dk) and c's words 0-12 (staged);
-// block b >= 1 is c's words 17 b - 4 .. 17 b + 12; the tail block c's last TAIL words
-template <int K>
-__device__ __forceinline__ void j_decaps_staged(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk,
-                                                size_t hs, size_t n, uint64_t* __restrict__ stage,
-                                                uint64_t* __restrict__ kbar) {
-  constexpr int RW = RW_SHAKE256, NW = 4 + P<K>::CT / 8, NFULL = NW / RW, TAIL = NW % RW;
-  const int lane = threadIdx.x & 63;
-  const size_t rec0 = ((size_t)__builtin_amdgcn_readfirstlane((uint32_t)(hs >> 32)) << 32) |
-                      __builtin_amdgcn_readfirstlane((uint32_t)(hs - lane));
-  const uint8_t* wbase = ct + rec0 * P<K>::CT;
-  const uint32_t nrec = (uint32_t)(n - rec0 < 64 ? n - rec0 : 64);
-  KState s;
-  kzero(s);
-  {
-    const uint64_t* z = (const uint64_t*)(sk + (hs < n ? hs : rec0) * P<K>::SK + 768 * K + 64);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) kxor(s, w, z[w]);
-  }
-  stage_words<RW - 4, RW>(stage, wbase, P<K>::CT, 0, 4, nrec);
-#pragma unroll
-  for (int w = 4; w < RW; ++w) kxor(s, w, stage[lane * RW + w]);
-  gsync();
-  keccak_f(s);
-#pragma unroll 1
-  for (int b = 1; b < NFULL; ++b) {
-    stage_words<RW, RW>(stage, wbase, P<K>::CT, b * RW - 4, 0, nrec);
-#pragma unroll
-    for (int w = 0; w < RW; ++w) kxor(s, w, stage[lane * RW + w]);
-    gsync();
-    keccak_f(s);
-  }
-  if constexpr (TAIL > 0) {
-    stage_words<TAIL, RW>(stage, wbase, P<K>::CT, NFULL * RW - 4, 0, nrec);
-#pragma unroll
-    for (int w = 0; w < TAIL; ++w) kxor(s, w, stage[lane * RW + w]);
-  }
-  s.a[TAIL].lo ^= DS_SHAKE;
-  s.a[RW - 1].hi ^= 0x80000000u;
-  keccak_f(s);
-  if (hs >= n) return;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
-}
-
 // The Encaps front and G(m' || h) on a lane pair (keccak_pair.cuh: the even lane holds the low
 // halves of the state words, the odd lane the high halves) for chunks of at most QRK_PAIR_FRONT_MAX
 // handshakes: there the front's lane-per-handshake waves (one per SIMD at 2^14 handshakes) are the
@@ -2603,37 +2481,27 @@ struct RXofFixCoop {
 };
 template <int K>
 struct RFrontEnc {  // (K, r) = G(m || H(ek)), lane / handshake
-  static constexpr int LDS = QRK_FRONT_STAGE ? 4 * 64 * RW_SHA3_256 * 8 : 0, WPE = 1;
+  static constexpr int LDS = 0, WPE = 1;
   const uint8_t *pk, *coins;
   size_t n;
   uint8_t* ss;
   uint64_t* seeds;
   unsigned nb;
-  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
     const size_t hs = (size_t)vb * 256 + threadIdx.x;
-    if constexpr (QRK_FRONT_STAGE) {
-      if ((size_t)vb * 256 + (threadIdx.x & ~63u) >= n) return;  // whole wave past the end
-      front_encaps_staged<K>(pk, coins, hs, n, (uint64_t*)lds + (threadIdx.x >> 6) * 64 * RW_SHA3_256, ss, seeds);
-    } else if (hs < n) {
-      front_encaps_hs<K>(pk, coins, hs, ss, seeds);
-    }
+    if (hs < n) front_encaps_hs<K>(pk, coins, hs, ss, seeds);
   }
 };
 template <int K>
 struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
-  static constexpr int LDS = QRK_FRONT_STAGE ? 4 * 64 * RW_SHAKE256 * 8 : 0, WPE = 1;
+  static constexpr int LDS = 0, WPE = 1;
   const uint8_t *ct, *sk;
   size_t n;
   uint64_t* kbar;
   unsigned nb;
-  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
     const size_t hs = (size_t)vb * 256 + threadIdx.x;
-    if constexpr (QRK_FRONT_STAGE) {
-      if ((size_t)vb * 256 + (threadIdx.x & ~63u) >= n) return;  // whole wave past the end
-      j_decaps_staged<K>(ct, sk, hs, n, (uint64_t*)lds + (threadIdx.x >> 6) * 64 * RW_SHAKE256, kbar);
-    } else if (hs < n) {
-      j_decaps_hs<K>(ct, sk, hs, kbar);
-    }
+    if (hs < n) j_decaps_hs<K>(ct, sk, hs, kbar);
   }
 };
 // lane-pair forms of two sponge roles (keccak_pair.cuh), 128 handshakes per workgroup
