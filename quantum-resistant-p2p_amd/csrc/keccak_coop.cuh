@@ -29,10 +29,6 @@
 
 #include "keccak.cuh"
 
-#ifndef QRK_COOP_ONESEL
-#define QRK_COOP_ONESEL 0
-#endif
-
 namespace qrk {
 
 // This layout against the round-1 one (lane y + 8x, C[x -/+ 1] by ds_bpermute, two LDS round trips
@@ -50,7 +46,6 @@ struct Coop {
   int g0, g1, g2;   // ds_bpermute byte addresses of the chi inputs B[X][Y], B[X+1][Y], B[X+2][Y]
   uint32_t shift;   // rho: v_alignbit shift (32 - r mod 32) mod 32
   bool swap;        // rho: swap the halves first
-  uint32_t swm;     // all-ones where swap
   uint32_t m0;      // all-ones where iota applies (lane (0, 0) and its replica)
   bool hi_slots;    // slots 6, 7 (refreshed from slots 1, 2)
   uint32_t hsm;     // all-ones on slots 6, 7
@@ -82,7 +77,6 @@ __device__ __forceinline__ Coop coop_init() {
   const int n = r & 31;
   c.shift = (uint32_t)((32 - n) & 31);
   c.swap = (r >= 32) != (n == 0);  // alignbit by 0 returns the low operand: r = 0 needs the swap
-  c.swm = c.swap ? 0xFFFFFFFFu : 0u;
   return c;
 }
 
@@ -135,12 +129,7 @@ __device__ __forceinline__ void keccak_f_coop(uint32_t& lo, uint32_t& hi, const 
     const uint32_t pl = dpp_shl1(cl), ph = dpp_shl1(ch);
     lo = xor3(lo, ml, __builtin_amdgcn_alignbit(pl, ph, 31));
     hi = xor3(hi, mh, __builtin_amdgcn_alignbit(ph, pl, 31));
-#if QRK_COOP_ONESEL >= 2
-    // the selects as full-rate v_bitop3 (a v_cndmask with a lane mask is a half-rate VOP3)
-    const uint32_t sl = __builtin_amdgcn_bitop3_b32(c.swm, hi, lo, 0xCA), sh = __builtin_amdgcn_bitop3_b32(c.swm, lo, hi, 0xCA);
-#else
     const uint32_t sl = c.swap ? hi : lo, sh = c.swap ? lo : hi;
-#endif
     lo = __builtin_amdgcn_alignbit(sl, sh, c.shift);
     hi = __builtin_amdgcn_alignbit(sh, sl, c.shift);
     const uint32_t b0l = bperm(c.g0, lo), b0h = bperm(c.g0, hi);
@@ -149,17 +138,10 @@ __device__ __forceinline__ void keccak_f_coop(uint32_t& lo, uint32_t& hi, const 
     lo = (b0l ^ (~b1l & b2l)) ^ (KRC_LO[r] & c.m0);
     hi = (b0h ^ (~b1h & b2h)) ^ (KRC_HI[r] & c.m0);
     const uint32_t rl = dpp_shr5(lo), rh = dpp_shr5(hi);
-#if QRK_COOP_ONESEL
-    lo = __builtin_amdgcn_bitop3_b32(c.hsm, rl, lo, 0xCA);  // hsm ? rl : lo
-    hi = __builtin_amdgcn_bitop3_b32(c.hsm, rh, hi, 0xCA);
-    sl_ = lo;
-    sh_ = hi;
-#else
     sl_ = __builtin_amdgcn_bitop3_b32(c.hsm, rl, lo, 0xCA);  // hsm ? rl : lo
     sh_ = __builtin_amdgcn_bitop3_b32(c.hsm, rh, hi, 0xCA);
     lo = c.hi_slots ? rl : lo;
     hi = c.hi_slots ? rh : hi;
-#endif
   }
 }
 
