@@ -177,3 +177,31 @@ def test_context_on_other_device_restores_current():
     assert torch.cuda.current_device() == 0
     assert bool((eng.decaps(sk, ct_) == ss).all())
     assert torch.cuda.current_device() == 0
+
+
+def test_set_chunk_concurrent_with_effective_chunk():
+    """qrk_ctx_set_chunk writes the chunk size under the context lock, as qrk_ctx_effective_chunk
+    reads it: threads setting two sizes while others read never see any other value."""
+    import threading
+
+    from qrkem._native import LIB
+    from qrkem.batch import BatchKEM
+    eng = BatchKEM(ALG, device=0)
+    sizes = (1 << 12, (1 << 20) + 64 * 3)
+    seen, stop = set(), threading.Event()
+
+    def setter(k):
+        for i in range(4000):
+            LIB.qrk_ctx_set_chunk(eng._ctx, sizes[(i + k) & 1])
+        stop.set()
+
+    def reader():
+        while not stop.is_set():
+            seen.add(int(LIB.qrk_ctx_effective_chunk(eng._ctx, ALG.encode())))
+
+    ts = [threading.Thread(target=setter, args=(k,)) for k in range(2)] + [threading.Thread(target=reader) for _ in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert seen and seen <= set(sizes), seen
