@@ -156,6 +156,9 @@ struct qrk_ctx {
   uint32_t* hflag = nullptr;      // single-shot completion flag (fine-grained pinned) ...
   uint32_t* hflag_dev = nullptr;  // ... its device address
   uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
+  uint32_t* fixc = nullptr;       // ML-KEM SampleNTT fix-up counters of chunks <= 2^16 (Streams::fixc)
+  int fixp = 0;                   // the counter the next such chunk counts into
+  bool fixc_dirty = false;        // a chunk's launches failed after the parity flip: re-zero both
   uint32_t ticket = 0;
   bool flag_next = false;         // run_batch: hand the flag to the next launch
   const uint8_t* hin_next = nullptr;  // ... and the public input's host copy (a by-value kernel argument)
@@ -388,6 +391,20 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     }
     S.kg_cnt = ctx->kg_cnt;
   }
+  if (a.family == Family::MLKEM && op != Op::KEYPAIR) {
+    if (!ctx->fixc) {
+      hipError_t e = hipMalloc((void**)&ctx->fixc, 2 * sizeof(uint32_t));
+      if (e == hipSuccess) e = hipMemset(ctx->fixc, 0, 2 * sizeof(uint32_t));
+      if (e != hipSuccess) return hip_fail("hipMalloc(fixc)", e);
+    }
+    if (ctx->fixc_dirty) {
+      const hipError_t e = hipMemsetAsync(ctx->fixc, 0, 2 * sizeof(uint32_t), st);
+      if (e != hipSuccess) return hip_fail("hipMemsetAsync(fixc)", e);
+      ctx->fixc_dirty = false;
+    }
+    S.fixc = ctx->fixc;
+    S.fixp = &ctx->fixp;
+  }
   TimerScope timer_scope(ctx->profiling ? &ctx->timer : nullptr);
   HT(3);
   for (size_t off = 0; off < n; off += chunk) {
@@ -448,7 +465,10 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
     }
     HT(4);
     if (e == hipSuccess) e = g_launch_err;
-    if (e != hipSuccess) return hip_fail("kernel launch", e);
+    if (e != hipSuccess) {
+      ctx->fixc_dirty = S.fixc != nullptr;  // the counters' zero-between-calls invariant is unknown now
+      return hip_fail("kernel launch", e);
+    }
     // key material of this chunk (seeds, m', K', Kbar, ...) does not outlive the call
     e = cleanse_records(a, m, ctx->scratch, st);
     if (e != hipSuccess) return hip_fail("hipMemsetAsync(cleanse)", e);
@@ -820,6 +840,7 @@ void qrk_ctx_destroy(qrk_ctx* ctx) {
   if (ctx->dstage) (void)hipFree(ctx->dstage);
   if (ctx->hstage) (void)hipHostFree(ctx->hstage);
   if (ctx->kg_cnt) (void)hipFree(ctx->kg_cnt);
+  if (ctx->fixc) (void)hipFree(ctx->fixc);
   if (ctx->ev_up) (void)hipEventDestroy(ctx->ev_up);
   if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
   delete ctx;

@@ -381,6 +381,7 @@ struct XofArgs {
   size_t rho_stride, n, C;
   XUnit* out;
   uint32_t *fix, *nfix;  // the fix-up list and its counter
+  uint32_t* zero_next;   // main pass (chunks <= DIRECT_RHO_MAX): the counter the next call counts into
 };
 // block vb of nvb (FIX: the grid-stride walk over the list uses nvb)
 template <int K, bool FIX>
@@ -388,6 +389,7 @@ __device__ __forceinline__ void xof_body(const XofArgs<K, FIX>& a, unsigned vb, 
   const uint32_t rb = ((threadIdx.x >> 6) * 16 * 64 + (threadIdx.x & 63)) * 4;  // ring_all: [wave][16][64]
   char* ring = (char*)ring_all;
   if constexpr (!FIX) {
+    if (vb == 0 && threadIdx.x == 0 && a.zero_next) *a.zero_next = 0u;
     const size_t e = (size_t)vb * 256 + threadIdx.x, hs = e % a.C;
     if (e >= (size_t)K * K * a.C || hs >= a.n) return;
     const int xy = (int)(e / a.C);
@@ -537,6 +539,52 @@ __device__ __forceinline__ void g_decaps_hs(const uint8_t* __restrict__ sk, cons
   for (int w = 0; w < 4; ++w) {
     kprime[hs * 4 + w] = kword(s, w);
     seeds[hs * 4 + w] = kword(s, 4 + w);
+  }
+}
+// J(z || c) split over two launches (chunks <= QRK_PAIR_FRONT_MAX): permutations [p0, p1) of its
+// J_PERMS, the sponge state kept between the two parts in scratch (jst: 25 words per handshake,
+// 64-handshake tiles; secret-derived, inside the records span the cleanse wipes).
+template <int K>
+struct JSplit {
+  static constexpr int NW = 4 + P<K>::CT / 8, NFULL = NW / RW_SHAKE256, TAIL = NW % RW_SHAKE256, PERMS = NFULL + 1;
+  static constexpr int P1 = PERMS - 2;  // the first launch's share; the last two ride with the fix-up / PRFs
+};
+template <int K>
+__device__ __forceinline__ void j_decaps_part(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk, size_t hs,
+                                              uint64_t* __restrict__ jst, uint64_t* __restrict__ kbar, int p0, int p1) {
+  using J = JSplit<K>;
+  const uint64_t* z = (const uint64_t*)(sk + hs * P<K>::SK + 768 * K + 64);
+  const uint64_t* c = (const uint64_t*)(ct + hs * P<K>::CT);
+  auto ld = [&](int w) { return w < 4 ? z[w] : c[w - 4]; };
+  KState s;
+  if (p0 == 0) {
+    kzero(s);
+  } else {
+#pragma unroll
+    for (int w = 0; w < 25; ++w) {
+      const uint64_t v = jst[tidx(hs, w, 25)];
+      s.a[w].lo = (uint32_t)v;
+      s.a[w].hi = (uint32_t)(v >> 32);
+    }
+  }
+  const int full_end = p1 < J::NFULL ? p1 : J::NFULL;
+#pragma unroll 1
+  for (int b = p0; b < full_end; ++b) {
+#pragma unroll
+    for (int w = 0; w < RW_SHAKE256; ++w) kxor(s, w, ld(b * RW_SHAKE256 + w));
+    keccak_f(s);
+  }
+  if (p1 == J::PERMS) {
+#pragma unroll
+    for (int w = 0; w < J::TAIL; ++w) kxor(s, w, ld(J::NFULL * RW_SHAKE256 + w));
+    s.a[J::TAIL].lo ^= DS_SHAKE;
+    s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
+    keccak_f(s);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
+  } else {
+#pragma unroll
+    for (int w = 0; w < 25; ++w) jst[tidx(hs, w, 25)] = kword(s, w);
   }
 }
 template <int K>
@@ -1070,13 +1118,13 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 
 // Scratch carve-up for a chunk of C handshakes
 struct ScratchView {
-  uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
+  uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar, *jst;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks, capacity K^2 C), its counter
   uint64_t* rho;         // every handshake's rho, 32 B apart (k_rho_copy)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 16) / 2 + 4 +
-         4 * C;
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + 25 * C + ((size_t)K * K * C + 16) / 2 +
+         4 + 4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -1093,6 +1141,8 @@ inline ScratchView carve(void* base, int K, size_t C) {
   p += 4 * C;
   v.kbar = p;
   p += 4 * C;
+  v.jst = p;
+  p += 25 * C;
   v.nfix = (uint32_t*)p;
   v.fix = v.nfix + 16;
   p += ((size_t)K * K * C + 16) / 2 + 4;
@@ -1346,7 +1396,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 }
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K, int TW = 64>
-__device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
+__device__ __forceinline__ uint32_t decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
@@ -1386,6 +1436,7 @@ __device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restr
     bits |= (uint32_t)compress_f<1>(i2f(decompress<DV>(v.v[t])) - w.v[t]) << t;
   }
   if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
+  return bits;  // m' bytes 2L, 2L + 1
 }
 
 // ============================================================ small batches: one launch per operation
@@ -2504,6 +2555,19 @@ struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
     if (hs < n) j_decaps_hs<K>(ct, sk, hs, kbar);
   }
 };
+template <int K>
+struct RJDecPart {  // permutations [p0, p1) of J(z || c), lane / handshake (JSplit)
+  static constexpr int LDS = 0, WPE = 1;
+  const uint8_t *ct, *sk;
+  size_t n;
+  uint64_t *jst, *kbar;
+  int p0, p1;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char*) const {
+    const size_t hs = (size_t)vb * 256 + threadIdx.x;
+    if (hs < n) j_decaps_part<K>(ct, sk, hs, jst, kbar, p0, p1);
+  }
+};
 // lane-pair forms of two sponge roles (keccak_pair.cuh), 128 handshakes per workgroup
 #ifndef QRK_PAIR_FRONT_MAX
 #define QRK_PAIR_FRONT_MAX (1 << 15)
@@ -2584,6 +2648,43 @@ struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
   }
 };
 
+// Chunks <= QRK_PAIR_FRONT_MAX: K-PKE.Decrypt, then G(m' || h) on lanes 0-1 of the same 16-lane
+// group (keccak_pair.cuh), m' handed over in the group's LDS: the decrypt role is not the critical
+// path of {J, decrypt, SampleNTT}, and the separate k_g_decaps launch (~9 us at 2^14 handshakes,
+// for ~2 us of work) goes away.
+template <int K>
+struct RDecryptG {
+  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = 1;
+  size_t n;
+  const uint8_t *ct, *sk;
+  uint64_t *mprime, *seeds, *kprime;
+  unsigned nb;
+  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
+    const int gi = threadIdx.x >> 4, L = threadIdx.x & 15;
+    GroupLds& g = ((GroupLds*)lds)[gi];
+    const size_t hs = (size_t)vb * GROUPS + gi;
+    const uint32_t bits = decrypt_core_hs<K>(n, ct, sk, mprime, hs, L, g);
+    ((uint16_t*)g.raw)[L] = (uint16_t)bits;
+    gsync();
+    if (hs < n && L < 2) {
+      const uint32_t* m32 = (const uint32_t*)g.raw;
+      const uint32_t* h = (const uint32_t*)(sk + hs * P<K>::SK + 768 * K + 32);
+      const int half = L;
+      const uint32_t hm = half ? 0xFFFFFFFFu : 0u;
+      PState st;
+      pzero(st);
+      pabsorb<RW_SHA3_512, 8, DS_SHA3>(st, hm, [&](int w) { return w < 4 ? m32[2 * w + half] : h[2 * (w - 4) + half]; });
+      uint32_t* kp = (uint32_t*)(kprime + hs * 4);
+      uint32_t* sd = (uint32_t*)(seeds + hs * 4);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        kp[2 * w + half] = st.a[w];
+        sd[2 * w + half] = st.a[4 + w];
+      }
+    }
+  }
+};
+
 template <int K, int MODE>
 struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and select), 16 lanes / hs
   static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = K == 4 ? 1 : 3;
@@ -2661,14 +2762,31 @@ void launch_multi(const char* name, std::initializer_list<const char*> names, co
 // SampleNTT roles for a chunk of C handshakes (n used): the main pass and its fix-up.  The fix-up
 // covers fix-up rates up to 1/64 (~0.7 % expected) in a single pass, one lane per listed entry:
 // it is latency-bound (4+ sequential permutations per lane), a second grid-stride pass would double it.
+// Where SampleNTT reads rho and counts its fix-up entries: the compact copy in scratch and the
+// scratch counter (k_rho_copy zeroes it), or -- chunks <= DIRECT_RHO_MAX -- rho in the keys
+// themselves and one of the context's two fix-up counters (Streams::fixc), the main pass zeroing
+// the other one for the next call: no k_rho_copy launch.
+struct RhoSrc {
+  const uint8_t* base;
+  size_t stride;
+  uint32_t *nfix, *zero_next;
+};
+template <int K>
+RXof<K, false> xof_role(const RhoSrc& r, size_t n, size_t C, const ScratchView& v) {
+  return {{r.base, r.stride, n, C, (XUnit*)v.xof, v.fix, r.nfix, r.zero_next}, blocks_for((size_t)K * K * C)};
+}
+template <int K>
+RXof<K, true> fix_role(const RhoSrc& r, size_t n, size_t C, const ScratchView& v) {
+  return {{r.base, r.stride, n, C, (XUnit*)v.xof, v.fix, r.nfix, nullptr},
+          (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
+}
 template <int K>
 RXof<K, false> xof_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix}, blocks_for((size_t)K * K * C)};
+  return xof_role<K>(RhoSrc{rho, 32, v.nfix, nullptr}, n, C, v);
 }
 template <int K>
 RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
-          (unsigned)std::min<size_t>((size_t)K * K * C / (64 * 256) + 1, 4096)};
+  return fix_role<K>(RhoSrc{rho, 32, v.nfix, nullptr}, n, C, v);
 }
 // chunks up to this size run the fix-up one wave per entry (RXofFixCoop): below it the
 // lane-per-entry fix-up's latency shows past the PRFs it shares a launch with, above it the
@@ -2677,24 +2795,39 @@ RXof<K, true> fix_role(const uint8_t* rho, size_t n, size_t C, const ScratchView
 // 2^16 -3.1 %, 2^17 -4.2 %.
 constexpr size_t COOP_FIX_MAX = (size_t)1 << 15;
 template <int K>
-RXofFixCoop<K> fix_coop_role(const uint8_t* rho, size_t n, size_t C, const ScratchView& v) {
-  return {{rho, 32, n, C, (XUnit*)v.xof, v.fix, v.nfix},
+RXofFixCoop<K> fix_coop_role(const RhoSrc& r, size_t n, size_t C, const ScratchView& v) {
+  return {{r.base, r.stride, n, C, (XUnit*)v.xof, v.fix, r.nfix, nullptr},
           (unsigned)std::min<size_t>((size_t)K * K * C / 256 + 1, 4096)};  // waves for 1/64 of the entries
 }
 // {SampleNTT fix-up, PRFs}: the fix-up's workgroups first (grid order)
 template <int K, class Prf>
-void launch_fix_prf(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, const Prf& prf, const Streams& s) {
+void launch_fix_prf(const RhoSrc& r, size_t n, size_t C, const ScratchView& v, const Prf& prf, const Streams& s) {
   if (C <= COOP_FIX_MAX)
-    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_coop_role<K>(rho, n, C, v), prf);
+    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_coop_role<K>(r, n, C, v), prf);
   else
-    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(rho, n, C, v), prf);
+    launch_multi("k_xof_fix+k_prf", {"k_xof_fix", "k_prf"}, s, fix_role<K>(r, n, C, v), prf);
+}
+template <int K, class Prf>
+void launch_fix_prf(const uint8_t* rho, size_t n, size_t C, const ScratchView& v, const Prf& prf, const Streams& s) {
+  launch_fix_prf<K>(RhoSrc{rho, 32, v.nfix, nullptr}, n, C, v, prf, s);
 }
 
-// k_xof reads rho from the compact copy in scratch (k_rho_copy, or KeyGen's front kernel)
-inline const uint8_t* rho_copy(const uint8_t* keys_rho, size_t key_stride, size_t n, const ScratchView& v, hipStream_t st) {
-  QRK_LAUNCH("k_rho_copy", st, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, st, keys_rho, key_stride, n, v.rho,
-             v.nfix);
-  return (const uint8_t*)v.rho;
+// Chunks up to this size read rho straight from the keys: there the k_rho_copy launch (~5 us,
+// launch-bound) costs more than the strided rho reads it saves (64 cache lines per wave instead of
+// 16; at 2^20 handshakes those reads were 1.2 GB per k_xof launch, see k_rho_copy).
+constexpr size_t DIRECT_RHO_MAX = (size_t)1 << 16;
+// Encaps / Decaps rho source for a chunk of C handshakes: keys_rho = the first key's rho
+inline RhoSrc rho_source(const uint8_t* keys_rho, size_t key_stride, size_t n, size_t C, const ScratchView& v,
+                         const Streams& s) {
+  if (C <= DIRECT_RHO_MAX && s.fixc && s.fixp) {
+    const int p = *s.fixp;
+    *s.fixp = p ^ 1;  // the next call counts into the word this call's main pass zeroes
+    return {keys_rho, key_stride, s.fixc + p, s.fixc + (p ^ 1)};
+  }
+  // k_xof reads rho from the compact copy in scratch
+  QRK_LAUNCH("k_rho_copy", s.main, k_rho_copy, dim3(blocks_for(4 * n)), dim3(256), 0, s.main, keys_rho, key_stride,
+             n, v.rho, v.nfix);
+  return {(const uint8_t*)v.rho, 32, v.nfix, nullptr};
 }
 
 // QRK_DEBUG_POISON (environment, tests / tools only): fill the sampled-matrix region with 0xFF
@@ -2758,7 +2891,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   }
   hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
-  const uint8_t* rho = rho_copy(pk + 384 * K, (size_t)P<K>::PK, n, v, st);
+  const RhoSrc rho = rho_source(pk + 384 * K, (size_t)P<K>::PK, n, C, v, s);
   const RFrontEnc<K> front{pk, coins, n, ss, v.seeds, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
@@ -2791,7 +2924,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   hipStream_t st = s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
   poison_xof<K>(C, v, st);
-  const uint8_t* rho = rho_copy(sk + 768 * K, (size_t)P<K>::SK, n, v, st);
+  const RhoSrc rho = rho_source(sk + 768 * K, (size_t)P<K>::SK, n, C, v, s);
   const RDecrypt<K> dec{n, ct, sk, v.mprime, gblocks};
   const RJDec<K> jd{ct, sk, n, v.kbar, blocks_for(n)};
   const RGDec<K> gd{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(n)};
@@ -2801,10 +2934,23 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   if (C <= QRK_PAIR_FRONT_MAX) {
     // J stays one lane per handshake: its launch, {J, decrypt core, SampleNTT}, is throughput-bound at
     // these sizes, and J on lane pairs (1.3x the issue slots) ran it 105.3 -> 118.7 us at 2^14
-    // (47.2e6 against 45.5e6 handshakes/s, profiles/r5/pair_fronts/abx_2p14_pairJ_noJ_off.jsonl)
-    launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
-                 xof_role<K>(rho, n, C, v));
-    launch_one("k_g_decaps", RGDecPair<K>{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(2 * n)}, s);
+    // (47.2e6 against 45.5e6 handshakes/s, profiles/r5/pair_fronts/abx_2p14_pairJ_noJ_off.jsonl).
+    // G(m' || h) runs in the decrypt role's groups (RDecryptG): no k_g_decaps launch.  J itself is split:
+    // its last two permutations run beside the fix-up and the PRFs (J's nine sequential permutations,
+    // ~89 us on their own at 2^14, were the critical path of this launch).
+    using J = JSplit<K>;
+    launch_multi("k_j_decaps_a+k_decrypt_g+k_xof", {"k_j_decaps_a", "k_decrypt_g", "k_xof"}, s,
+                 RJDecPart<K>{ct, sk, n, v.jst, v.kbar, 0, J::P1, blocks_for(n)},
+                 RDecryptG<K>{n, ct, sk, v.mprime, v.seeds, v.kprime, gblocks}, xof_role<K>(rho, n, C, v));
+    const RJDecPart<K> j2{ct, sk, n, v.jst, v.kbar, J::P1, J::PERMS, blocks_for(n)};
+    if (C <= COOP_FIX_MAX)
+      launch_multi("k_xof_fix+k_j_decaps_b+k_prf", {"k_xof_fix", "k_j_decaps_b", "k_prf"}, s,
+                   fix_coop_role<K>(rho, n, C, v), j2, prf);
+    else
+      launch_multi("k_xof_fix+k_j_decaps_b+k_prf", {"k_xof_fix", "k_j_decaps_b", "k_prf"}, s, fix_role<K>(rho, n, C, v),
+                   j2, prf);
+    launch_one("k_encrypt_core", core, s);
+    return hipGetLastError();
   } else {
     launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
                  xof_role<K>(rho, n, C, v));
@@ -2830,10 +2976,11 @@ size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }
 
 void mlkem_records_span(const AlgInfo& a, size_t C, size_t* off, size_t* bytes) {
-  // mlkem::carve: the sampled matrix, the PRF words, then seeds | m' | K' | Kbar (4 C words each)
+  // mlkem::carve: the sampled matrix, the PRF words, then seeds | m' | K' | Kbar (4 C words each) | the
+  // split J sponge state (25 C words)
   const size_t K = (size_t)a.k;
   *off = (K * K * C * mlkem::XOF_W + (2 * K + 1) * C * mlkem::PRF_W) * sizeof(uint64_t);
-  *bytes = 16 * C * sizeof(uint64_t);
+  *bytes = 41 * C * sizeof(uint64_t);
 }
 
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
@@ -2841,7 +2988,7 @@ hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t 
   if (n == 0 || n <= QRK_SMALL_MAX) return hipSuccess;
   const size_t C = mlkem::round64(n);
   const mlkem::ScratchView v = mlkem::carve(scratch, a.k, C);
-  return hipMemsetAsync(v.seeds, 0, 16 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar
+  return hipMemsetAsync(v.seeds, 0, 41 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar | jst
 }
 
 hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,
