@@ -172,8 +172,7 @@ def mlkem_core_ops(k, eta1, kind):
     raise ValueError(kind)
 
 
-ONE_OP_KERNELS = {"k_front_encaps", "k_j_decaps", "k_g_decaps", "k_decrypt_core", "k_front_decaps", "k_j_decaps_a",
-                  "k_j_decaps_b", "k_decrypt_g"}
+ONE_OP_KERNELS = {"k_front_encaps", "k_j_decaps", "k_g_decaps", "k_decrypt_core", "k_front_decaps"}
 
 
 def kernel_ops_per_hs(alg, name, mode, calls=None):
@@ -185,7 +184,7 @@ def kernel_ops_per_hs(alg, name, mode, calls=None):
     `calls` overrides how many of the step's operations run a shared kernel."""
     if "+" in name:
         roles = name.split("+")
-        c = 1 if any(r in ONE_OP_KERNELS for r in roles) else calls
+        c = 1 if any(r in ONE_OP_KERNELS for r in roles) else None
         parts = [kernel_ops_per_hs(alg, r, mode, c) for r in roles]
         ops = [o for o, _ in parts if o is not None]
         bounds = {b for o, b in parts if o is not None}
@@ -227,13 +226,8 @@ def kernel_ops_per_hs(alg, name, mode, calls=None):
         return (1 + (32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
     if name == "k_j_decaps":  # J(z || c)
         return ((32 + ct + 1 + 135) // 136) * PERM_OPS, "valu"
-    if name in ("k_j_decaps_a", "k_j_decaps_b"):  # J split over two launches (chunks <= 2^15): all but
-        perms = (32 + ct + 1 + 135) // 136          # the last two permutations, then those two
-        return ((perms - 2) if name == "k_j_decaps_a" else 2) * PERM_OPS, "valu"
     if name == "k_g_decaps":  # G(m' || h)
         return PERM_OPS, "valu"
-    if name == "k_decrypt_g":  # K-PKE.Decrypt with G(m' || h) in its groups (chunks <= 2^15)
-        return mlkem_core_ops(k, eta1, "decrypt") + PERM_OPS, "valu"
     if name == "k_prf":
         return calls * (k * (1 if eta1 == 2 else 2) + (k + 1)) * PERM_OPS, "valu"
     if name == "k_encrypt_core":  # Encaps' Encrypt, and Decaps' re-encryption
@@ -448,12 +442,8 @@ def kernel_report(alg, mode, prof, B):
     (HIP-event durations).  Returns (kernels, roofline-of-dominant, mfma-object-or-None)."""
     kernels = {}
     tot_ms = sum(ms for ms, _ in prof.values()) or 1.0
-    # chunks <= 2^15: Decaps runs its own {fix-up, J's last permutations, PRFs} launch, so the plain
-    # {fix-up, PRFs} launch is Encaps' alone (once per step)
-    split = any("k_j_decaps_b" in k for k in prof)
-    calls_of = lambda k: 1 if split and k == "k_xof_fix+k_prf" else None  # noqa: E731
     for name, (ms, cnt) in prof.items():
-        ops, bound = kernel_ops_per_hs(alg, name, mode, calls_of(name))
+        ops, bound = kernel_ops_per_hs(alg, name, mode)
         kernels[name] = {"avg_ms": ms / cnt, "launches": cnt, "share": ms / tot_ms}
         if ops is not None:
             rate = ops * B / (ms * 1e-3)
@@ -465,7 +455,7 @@ def kernel_report(alg, mode, prof, B):
     roof, mfma = None, None
     if prof:
         dom = max(prof, key=lambda k: prof[k][0])
-        ops, bound = kernel_ops_per_hs(alg, dom, mode, calls_of(dom))
+        ops, bound = kernel_ops_per_hs(alg, dom, mode)
         ms, cnt = prof[dom]
         if ops is not None:
             achieved = ops * B / (ms * 1e-3)

@@ -156,7 +156,7 @@ struct qrk_ctx {
   uint32_t* hflag = nullptr;      // single-shot completion flag (fine-grained pinned) ...
   uint32_t* hflag_dev = nullptr;  // ... its device address
   uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
-  uint32_t* fixc = nullptr;       // ML-KEM SampleNTT fix-up counters of chunks <= 2^16 (Streams::fixc)
+  uint32_t* fixc = nullptr;       // ML-KEM SampleNTT fix-up counters of chunks <= 2^15 (Streams::fixc)
   int fixp = 0;                   // the counter the next such chunk counts into
   bool fixc_dirty = false;        // a chunk's launches failed after the parity flip: re-zero both
   uint32_t ticket = 0;

@@ -541,52 +541,6 @@ __device__ __forceinline__ void g_decaps_hs(const uint8_t* __restrict__ sk, cons
     seeds[hs * 4 + w] = kword(s, 4 + w);
   }
 }
-// J(z || c) split over two launches (chunks <= QRK_PAIR_FRONT_MAX): permutations [p0, p1) of its
-// J_PERMS, the sponge state kept between the two parts in scratch (jst: 25 words per handshake,
-// 64-handshake tiles; secret-derived, inside the records span the cleanse wipes).
-template <int K>
-struct JSplit {
-  static constexpr int NW = 4 + P<K>::CT / 8, NFULL = NW / RW_SHAKE256, TAIL = NW % RW_SHAKE256, PERMS = NFULL + 1;
-  static constexpr int P1 = PERMS - 2;  // the first launch's share; the last two ride with the fix-up / PRFs
-};
-template <int K>
-__device__ __forceinline__ void j_decaps_part(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk, size_t hs,
-                                              uint64_t* __restrict__ jst, uint64_t* __restrict__ kbar, int p0, int p1) {
-  using J = JSplit<K>;
-  const uint64_t* z = (const uint64_t*)(sk + hs * P<K>::SK + 768 * K + 64);
-  const uint64_t* c = (const uint64_t*)(ct + hs * P<K>::CT);
-  auto ld = [&](int w) { return w < 4 ? z[w] : c[w - 4]; };
-  KState s;
-  if (p0 == 0) {
-    kzero(s);
-  } else {
-#pragma unroll
-    for (int w = 0; w < 25; ++w) {
-      const uint64_t v = jst[tidx(hs, w, 25)];
-      s.a[w].lo = (uint32_t)v;
-      s.a[w].hi = (uint32_t)(v >> 32);
-    }
-  }
-  const int full_end = p1 < J::NFULL ? p1 : J::NFULL;
-#pragma unroll 1
-  for (int b = p0; b < full_end; ++b) {
-#pragma unroll
-    for (int w = 0; w < RW_SHAKE256; ++w) kxor(s, w, ld(b * RW_SHAKE256 + w));
-    keccak_f(s);
-  }
-  if (p1 == J::PERMS) {
-#pragma unroll
-    for (int w = 0; w < J::TAIL; ++w) kxor(s, w, ld(J::NFULL * RW_SHAKE256 + w));
-    s.a[J::TAIL].lo ^= DS_SHAKE;
-    s.a[RW_SHAKE256 - 1].hi ^= 0x80000000u;
-    keccak_f(s);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) kbar[hs * 4 + w] = kword(s, w);
-  } else {
-#pragma unroll
-    for (int w = 0; w < 25; ++w) jst[tidx(hs, w, 25)] = kword(s, w);
-  }
-}
 template <int K>
 __device__ __forceinline__ void j_decaps_hs(const uint8_t* __restrict__ ct, const uint8_t* __restrict__ sk, size_t hs,
                                             uint64_t* __restrict__ kbar) {
@@ -1118,13 +1072,13 @@ __device__ __forceinline__ uint32_t group_or(uint32_t x) {
 
 // Scratch carve-up for a chunk of C handshakes
 struct ScratchView {
-  uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar, *jst;
+  uint64_t *xof, *prf, *seeds, *mprime, *kprime, *kbar;
   uint32_t *fix, *nfix;  // SampleNTT fix-up list (entries needing > 3 blocks, capacity K^2 C), its counter
   uint64_t* rho;         // every handshake's rho, 32 B apart (k_rho_copy)
 };
 __host__ __device__ inline size_t scratch_words(int K, size_t C) {
-  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + 25 * C + ((size_t)K * K * C + 16) / 2 +
-         4 + 4 * C;
+  return (size_t)K * K * C * XOF_W + (size_t)(2 * K + 1) * C * PRF_W + 16 * C + ((size_t)K * K * C + 16) / 2 + 4 +
+         4 * C;
 }
 inline ScratchView carve(void* base, int K, size_t C) {
   ScratchView v;
@@ -1141,8 +1095,6 @@ inline ScratchView carve(void* base, int K, size_t C) {
   p += 4 * C;
   v.kbar = p;
   p += 4 * C;
-  v.jst = p;
-  p += 25 * C;
   v.nfix = (uint32_t*)p;
   v.fix = v.nfix + 16;
   p += ((size_t)K * K * C + 16) / 2 + 4;
@@ -1396,7 +1348,7 @@ __device__ __forceinline__ void encrypt_core_hs(size_t n, size_t C, const uint64
 }
 // ------------------------------------------------------------ K-PKE.Decrypt core
 template <int K, int TW = 64>
-__device__ __forceinline__ uint32_t decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
+__device__ __forceinline__ void decrypt_core_hs(size_t n, const uint8_t* __restrict__ ct,
                                                       const uint8_t* __restrict__ sk, uint64_t* __restrict__ mprime, size_t hs_raw, int L, GroupLds& g) {
   constexpr int DU = P<K>::DU, DV = P<K>::DV;
   const bool active = hs_raw < n;
@@ -1436,7 +1388,6 @@ __device__ __forceinline__ uint32_t decrypt_core_hs(size_t n, const uint8_t* __r
     bits |= (uint32_t)compress_f<1>(i2f(decompress<DV>(v.v[t])) - w.v[t]) << t;
   }
   if (active) ((uint16_t*)(mprime + (TW == 64 ? hs : 0) * 4))[L] = (uint16_t)bits;
-  return bits;  // m' bytes 2L, 2L + 1
 }
 
 // ============================================================ small batches: one launch per operation
@@ -2555,19 +2506,6 @@ struct RJDec {  // Kbar = J(z || c), lane / handshake: needs only the inputs
     if (hs < n) j_decaps_hs<K>(ct, sk, hs, kbar);
   }
 };
-template <int K>
-struct RJDecPart {  // permutations [p0, p1) of J(z || c), lane / handshake (JSplit)
-  static constexpr int LDS = 0, WPE = 1;
-  const uint8_t *ct, *sk;
-  size_t n;
-  uint64_t *jst, *kbar;
-  int p0, p1;
-  unsigned nb;
-  __device__ __forceinline__ void run(unsigned vb, char*) const {
-    const size_t hs = (size_t)vb * 256 + threadIdx.x;
-    if (hs < n) j_decaps_part<K>(ct, sk, hs, jst, kbar, p0, p1);
-  }
-};
 // lane-pair forms of two sponge roles (keccak_pair.cuh), 128 handshakes per workgroup
 #ifndef QRK_PAIR_FRONT_MAX
 #define QRK_PAIR_FRONT_MAX (1 << 15)
@@ -2645,43 +2583,6 @@ struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
   __device__ __forceinline__ void run(unsigned vb, char* lds) const {
     const int gi = threadIdx.x >> 4;
     decrypt_core_hs<K>(n, ct, sk, mprime, (size_t)vb * GROUPS + gi, threadIdx.x & 15, ((GroupLds*)lds)[gi]);
-  }
-};
-
-// Chunks <= QRK_PAIR_FRONT_MAX: K-PKE.Decrypt, then G(m' || h) on lanes 0-1 of the same 16-lane
-// group (keccak_pair.cuh), m' handed over in the group's LDS: the decrypt role is not the critical
-// path of {J, decrypt, SampleNTT}, and the separate k_g_decaps launch (~9 us at 2^14 handshakes,
-// for ~2 us of work) goes away.
-template <int K>
-struct RDecryptG {
-  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = 1;
-  size_t n;
-  const uint8_t *ct, *sk;
-  uint64_t *mprime, *seeds, *kprime;
-  unsigned nb;
-  __device__ __forceinline__ void run(unsigned vb, char* lds) const {
-    const int gi = threadIdx.x >> 4, L = threadIdx.x & 15;
-    GroupLds& g = ((GroupLds*)lds)[gi];
-    const size_t hs = (size_t)vb * GROUPS + gi;
-    const uint32_t bits = decrypt_core_hs<K>(n, ct, sk, mprime, hs, L, g);
-    ((uint16_t*)g.raw)[L] = (uint16_t)bits;
-    gsync();
-    if (hs < n && L < 2) {
-      const uint32_t* m32 = (const uint32_t*)g.raw;
-      const uint32_t* h = (const uint32_t*)(sk + hs * P<K>::SK + 768 * K + 32);
-      const int half = L;
-      const uint32_t hm = half ? 0xFFFFFFFFu : 0u;
-      PState st;
-      pzero(st);
-      pabsorb<RW_SHA3_512, 8, DS_SHA3>(st, hm, [&](int w) { return w < 4 ? m32[2 * w + half] : h[2 * (w - 4) + half]; });
-      uint32_t* kp = (uint32_t*)(kprime + hs * 4);
-      uint32_t* sd = (uint32_t*)(seeds + hs * 4);
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        kp[2 * w + half] = st.a[w];
-        sd[2 * w + half] = st.a[4 + w];
-      }
-    }
   }
 };
 
@@ -2815,7 +2716,7 @@ void launch_fix_prf(const uint8_t* rho, size_t n, size_t C, const ScratchView& v
 // Chunks up to this size read rho straight from the keys: there the k_rho_copy launch (~5 us,
 // launch-bound) costs more than the strided rho reads it saves (64 cache lines per wave instead of
 // 16; at 2^20 handshakes those reads were 1.2 GB per k_xof launch, see k_rho_copy).
-constexpr size_t DIRECT_RHO_MAX = (size_t)1 << 16;
+constexpr size_t DIRECT_RHO_MAX = (size_t)1 << 15;
 // Encaps / Decaps rho source for a chunk of C handshakes: keys_rho = the first key's rho
 inline RhoSrc rho_source(const uint8_t* keys_rho, size_t key_stride, size_t n, size_t C, const ScratchView& v,
                          const Streams& s) {
@@ -2931,31 +2832,17 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
-  if (C <= QRK_PAIR_FRONT_MAX) {
-    // J stays one lane per handshake: its launch, {J, decrypt core, SampleNTT}, is throughput-bound at
-    // these sizes, and J on lane pairs (1.3x the issue slots) ran it 105.3 -> 118.7 us at 2^14
-    // (47.2e6 against 45.5e6 handshakes/s, profiles/r5/pair_fronts/abx_2p14_pairJ_noJ_off.jsonl).
-    // G(m' || h) runs in the decrypt role's groups (RDecryptG): no k_g_decaps launch.  J itself is split:
-    // its last two permutations run beside the fix-up and the PRFs (J's nine sequential permutations,
-    // ~89 us on their own at 2^14, were the critical path of this launch).
-    using J = JSplit<K>;
-    launch_multi("k_j_decaps_a+k_decrypt_g+k_xof", {"k_j_decaps_a", "k_decrypt_g", "k_xof"}, s,
-                 RJDecPart<K>{ct, sk, n, v.jst, v.kbar, 0, J::P1, blocks_for(n)},
-                 RDecryptG<K>{n, ct, sk, v.mprime, v.seeds, v.kprime, gblocks}, xof_role<K>(rho, n, C, v));
-    const RJDecPart<K> j2{ct, sk, n, v.jst, v.kbar, J::P1, J::PERMS, blocks_for(n)};
-    if (C <= COOP_FIX_MAX)
-      launch_multi("k_xof_fix+k_j_decaps_b+k_prf", {"k_xof_fix", "k_j_decaps_b", "k_prf"}, s,
-                   fix_coop_role<K>(rho, n, C, v), j2, prf);
-    else
-      launch_multi("k_xof_fix+k_j_decaps_b+k_prf", {"k_xof_fix", "k_j_decaps_b", "k_prf"}, s, fix_role<K>(rho, n, C, v),
-                   j2, prf);
-    launch_one("k_encrypt_core", core, s);
-    return hipGetLastError();
-  } else {
-    launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
-                 xof_role<K>(rho, n, C, v));
+  // J stays one lane per handshake: at chunks <= 2^15 its launch, {J, decrypt core, SampleNTT}, is
+  // throughput-bound, and J on lane pairs (1.3x the issue slots) ran it 105.3 -> 118.7 us at 2^14
+  // (47.2e6 against 45.5e6 handshakes/s, profiles/r5/pair_fronts/abx_2p14_pairJ_noJ_off.jsonl); J split
+  // over this launch and the next (its last two permutations beside the fix-up and the PRFs) took
+  // 4 us off this launch and added 3-14 us to the next: no gain (profiles/r5/mid/)
+  launch_multi("k_j_decaps+k_decrypt_core+k_xof", {"k_j_decaps", "k_decrypt_core", "k_xof"}, s, jd, dec,
+               xof_role<K>(rho, n, C, v));
+  if (C <= QRK_PAIR_FRONT_MAX)
+    launch_one("k_g_decaps", RGDecPair<K>{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(2 * n)}, s);
+  else
     launch_one("k_g_decaps", gd, s);
-  }
   launch_fix_prf<K>(rho, n, C, v, prf, s);
   launch_one("k_encrypt_core", core, s);
   return hipGetLastError();
@@ -2976,11 +2863,10 @@ size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }
 
 void mlkem_records_span(const AlgInfo& a, size_t C, size_t* off, size_t* bytes) {
-  // mlkem::carve: the sampled matrix, the PRF words, then seeds | m' | K' | Kbar (4 C words each) | the
-  // split J sponge state (25 C words)
+  // mlkem::carve: the sampled matrix, the PRF words, then seeds | m' | K' | Kbar (4 C words each)
   const size_t K = (size_t)a.k;
   *off = (K * K * C * mlkem::XOF_W + (2 * K + 1) * C * mlkem::PRF_W) * sizeof(uint64_t);
-  *bytes = 41 * C * sizeof(uint64_t);
+  *bytes = 16 * C * sizeof(uint64_t);
 }
 
 hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st) {
@@ -2988,7 +2874,7 @@ hipError_t mlkem_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t 
   if (n == 0 || n <= QRK_SMALL_MAX) return hipSuccess;
   const size_t C = mlkem::round64(n);
   const mlkem::ScratchView v = mlkem::carve(scratch, a.k, C);
-  return hipMemsetAsync(v.seeds, 0, 41 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar | jst
+  return hipMemsetAsync(v.seeds, 0, 16 * C * sizeof(uint64_t), st);  // seeds | mprime | kprime | kbar
 }
 
 hipError_t mlkem_keypair(const AlgInfo& a, size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch,

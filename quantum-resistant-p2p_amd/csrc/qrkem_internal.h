@@ -99,7 +99,7 @@ struct Streams {
   // Decaps: c), passed as a kernel argument instead of read over PCIe.  Secret inputs are never
   // passed by value: the runtime's kernel-argument pool is not wiped.
   const uint8_t* host_in1 = nullptr;
-  // batched ML-KEM Encaps / Decaps at chunks <= 2^16: the context's two SampleNTT fix-up counters
+  // batched ML-KEM Encaps / Decaps at chunks <= 2^15: the context's two SampleNTT fix-up counters
   // (device, zero at allocation) and which one the next call counts into (host; the call flips it
   // and its first launch zeroes the other word, mlkem.hip rho_source)
   uint32_t* fixc = nullptr;

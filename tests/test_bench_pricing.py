@@ -44,21 +44,3 @@ def test_survey_w_pricing_of_the_cores():
     e = kernels["k_encrypt_core"]
     assert e["survey_w_frac"] == pytest.approx(e["frac"] * (2 * (7 * ntt + 12 * bm)) / bench.kernel_ops_per_hs(
         "ML-KEM-768", "k_encrypt_core", "encdec")[0])
-
-
-@pytest.mark.parametrize("alg,k", [("ML-KEM-512", 2), ("ML-KEM-768", 3), ("ML-KEM-1024", 4)])
-def test_small_chunk_schedule_prices_the_same_step(alg, k):
-    """Chunks <= 2^15: G(m' || h) inside the decrypt role, J split over Decaps' first two launches, and
-    Encaps' {fix-up, PRFs} launch once per step -- the step's total ops equal the large-chunk schedule's."""
-    ops = lambda name, mode="encdec", calls=None: bench.kernel_ops_per_hs(alg, name, mode, calls)[0]  # noqa: E731
-    assert ops("k_j_decaps_a") + ops("k_j_decaps_b") == ops("k_j_decaps")
-    assert ops("k_decrypt_g") == ops("k_decrypt_core") + ops("k_g_decaps")
-    small = (ops("k_front_encaps+k_xof") + ops("k_j_decaps_a+k_decrypt_g+k_xof") + ops("k_xof_fix+k_prf", calls=1)
-             + ops("k_xof_fix+k_j_decaps_b+k_prf") + ops("k_encrypt_core"))
-    large = (ops("k_front_encaps+k_xof") + ops("k_j_decaps+k_decrypt_core+k_xof") + ops("k_xof_fix+k_prf")
-             + ops("k_g_decaps") + ops("k_encrypt_core"))
-    assert small == large
-    prof = {"k_xof_fix+k_prf": (1.0, 1), "k_xof_fix+k_j_decaps_b+k_prf": (1.0, 1)}
-    kernels, _, _ = bench.kernel_report(alg, "encdec", prof, 1 << 14)
-    assert kernels["k_xof_fix+k_prf"]["achieved_Tops"] == pytest.approx(
-        kernels["k_xof_fix+k_j_decaps_b+k_prf"]["achieved_Tops"] - ops("k_j_decaps_b") * (1 << 14) / 1e-3 / 1e12)

@@ -316,3 +316,41 @@ def test_sample_ntt_fixup_resume_and_overflow(engines, alg, k, n):
     oct_, oss = orc.batch_encaps(alg, pk[idx], np.ascontiguousarray(ec[idx]), 8)
     assert np.array_equal(_host(ct)[idx], oct_)
     assert np.array_equal(_host(ss)[idx], oss)
+
+
+def test_fixup_counters_across_calls():
+    """Chunks of at most 2^15 read rho from the keys and count SampleNTT fix-ups into one of the
+    context's two counters, each call zeroing the other for the next (no k_rho_copy launch).  A run of
+    Encaps / Decaps calls whose every pk needs fix-ups -- direct-path chunks back to back, a call split
+    into several direct chunks, and copy-path chunks (> 2^15) in between -- stays byte-exact vs the
+    oracle on every call (Decaps with dk's copy of rho replaced too)."""
+    import oracle as orc
+    from qrkem.batch import BatchKEM
+    alg, k = "ML-KEM-768", 3
+    rng = np.random.default_rng(91)
+    for _ in range(4000):
+        rho = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        if sum(_sample_ntt_needs_4th_block(rho, i, j) for i in range(k) for j in range(k)) >= 1:
+            break
+    else:
+        pytest.fail("no rho with a 4-block SampleNTT entry found")
+    kc0 = np.ascontiguousarray(orc.bench_coins(1, 64, seed=91))
+    opk, osk = orc.batch_keypair(alg, kc0)
+    opk[:, -32:] = np.frombuffer(rho, dtype=np.uint8)
+    osk[:, 768 * k:768 * k + 32] = np.frombuffer(rho, dtype=np.uint8)  # dk's copy of ek's rho (H(ek) stale)
+    big = BatchKEM(alg, device=0)
+    small = BatchKEM(alg, device=0, chunk=2048)  # a 5000-handshake call = three direct-path chunks
+    for step, (eng, n) in enumerate([(big, 1100), (big, 3000), (small, 5000), (big, (1 << 15) + 64), (big, 1500),
+                                     (small, 5000), (big, 2000)]):
+        coins = orc.bench_coins(n, 32, seed=300 + step)
+        pk = np.repeat(opk, n, axis=0)
+        sk = np.repeat(osk, n, axis=0)
+        ct, ss = eng.encaps(_dev(pk), coins=_dev(coins))
+        ss2 = _host(eng.decaps(_dev(sk), ct))
+        ct, ss = _host(ct), _host(ss)
+        idx = np.unique(np.r_[np.arange(4), np.linspace(0, n - 1, 120).astype(int), n - 1])
+        oct_, oss = orc.batch_encaps(alg, pk[idx], np.ascontiguousarray(coins[idx]))
+        assert np.array_equal(ct[idx], oct_), (step, n)
+        assert np.array_equal(ss[idx], oss), (step, n)
+        # Decaps re-encrypts under the same fix-up-heavy rho (its implicit-rejection outcome as the oracle's)
+        assert np.array_equal(ss2[idx], orc.batch_decaps(alg, sk[idx], np.ascontiguousarray(ct[idx]))), (step, n)

@@ -22,8 +22,8 @@ from pathlib import Path
 # ML-KEM role kernels (mlkem.hip k_multi / k_role; k_pair / k_tri in older builds): the rocprof name
 # carries the role types; the library's own launch names (QRK_LAUNCH, bench.py's kernel tables)
 # join the roles with '+'
-ROLES = {"RFrontEnc": "k_front_encaps", "RPrf": "k_prf", "RDecryptG": "k_decrypt_g", "RDecrypt": "k_decrypt_core",
-         "RJDecPart": "k_j_decaps_part", "RJDec": "k_j_decaps", "RGDec": "k_g_decaps", "RCore": "k_encrypt_core"}
+ROLES = {"RFrontEnc": "k_front_encaps", "RPrf": "k_prf", "RDecrypt": "k_decrypt_core", "RJDec": "k_j_decaps",
+         "RGDec": "k_g_decaps", "RCore": "k_encrypt_core"}
 
 
 def role_name(t: str) -> str:
@@ -50,10 +50,7 @@ def short(name: str) -> str:
             depth -= ch == ">"
             cur += ch
         args.append(cur)
-        names = [role_name(a) for a in args]
-        # the split J (chunks <= 2^15): its first part shares a launch with k_decrypt_g
-        part = "k_j_decaps_a" if "k_decrypt_g" in names else "k_j_decaps_b"
-        return "+".join(part if r == "k_j_decaps_part" else r for r in names)
+        return "+".join(role_name(a) for a in args)
     m = re.search(r"(k_\w+)(<[^(]*>)?\(", name)
     if not m:
         return name.split("(")[0][:60]
