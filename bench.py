@@ -122,7 +122,12 @@ def frodo_perms(alg):
 # HQC (n, n1, n2, w, w_r, w_e, k): the 2023-04-30 HQC parameter sets (oracle/py/hqc_spec.py)
 HQ = {"HQC-128": (17669, 46, 384, 66, 75, 75, 16), "HQC-192": (35851, 56, 640, 100, 114, 114, 24),
       "HQC-256": (57637, 90, 640, 131, 149, 149, 32)}
-# sparse-dense product in F2[X]/(X^n-1): one funnel shift + one XOR per (position, 32-bit word)
+# sparse-dense product in F2[X]/(X^n-1): one funnel shift + one XOR per (position, 32-bit word), and
+# the word's window read from LDS.  Per wave and position (64 output words): the reads are >= 64
+# dwords = 2 LDS clocks of the CU (128 B/clk), the VALU work one half-rate v_alignbit (4 SIMD clocks)
+# + one v_xor (2) = 1.5 CU clocks over its 4 SIMDs -- so the products are priced against the LDS
+# (LDS_LOOKUP_PEAK, one ds_read_b32 lane per word and position), with the VALU view kept beside it
+# (`valu_frac`).  The kernels read (WPT + 1) / WPT window words per output word (1.2 at WPT = 5).
 SPARSE_OPS = 2
 
 
@@ -200,7 +205,7 @@ def kernel_ops_per_hs(alg, name, mode, calls=None):
         if name in wk["perms"]:
             return c * wk["perms"][name] * PERM_OPS, "valu"
         if name in wk["ops"]:
-            return c * wk["ops"][name], "valu"
+            return c * wk["ops"][name] // SPARSE_OPS, "lds"  # LDS word reads (see SPARSE_OPS)
         return None, None
     if alg in FP:
         n = FP[alg][0]
@@ -449,6 +454,8 @@ def kernel_report(alg, mode, prof, B):
             rate = ops * B / (ms * 1e-3)
             peak = {"mfma": MFMA_I8_PEAK, "lds": LDS_LOOKUP_PEAK}.get(bound, VALU_PEAK)
             kernels[name].update(bound=bound, achieved_Tops=rate / 1e12, frac=rate / peak)
+            if alg in HQ and bound == "lds":  # the same product priced by its VALU ops
+                kernels[name]["valu_frac"] = rate * SPARSE_OPS / VALU_PEAK
             sw = survey_core_ops(alg, name, mode)
             if sw is not None:  # the same kernel priced by SURVEY.md 8d's W (NTT + basemul terms only)
                 kernels[name].update(survey_w_Tops=sw * B / (ms * 1e-3) / 1e12, survey_w_frac=sw * B / (ms * 1e-3) / peak)
@@ -465,6 +472,8 @@ def kernel_report(alg, mode, prof, B):
                         bound, "Top/s (int8 MFMA ops)"),
                     "frac": achieved / peak, "traffic": None,
                     "ops_per_launch": ops * B / cnt, "avg_launch_ms": ms / cnt}
+            if alg in HQ and bound == "lds":
+                roof["valu_frac"] = achieved * SPARSE_OPS / VALU_PEAK
         gk = "k_fr_gen_mm_aes" if "k_fr_gen_mm_aes" in prof else "k_fr_gen_mm"
         if gk in prof:
             # S'A runs on MFMA inside the fused Gen(A) kernel: its rate is priced over that

@@ -44,3 +44,16 @@ def test_survey_w_pricing_of_the_cores():
     e = kernels["k_encrypt_core"]
     assert e["survey_w_frac"] == pytest.approx(e["frac"] * (2 * (7 * ntt + 12 * bm)) / bench.kernel_ops_per_hs(
         "ML-KEM-768", "k_encrypt_core", "encdec")[0])
+
+
+def test_hqc_products_priced_against_lds():
+    """HQC's sparse-dense products are bound by their LDS window reads (>= 1 dword per output word and
+    position: 2 LDS clocks per wave-position against 1.5 CU clocks of VALU), so bench.py prices them
+    against LDS_LOOKUP_PEAK and reports the VALU fraction beside it."""
+    ops, bound = bench.kernel_ops_per_hs("HQC-128", "k_hqc_enc_mul", "encdec")
+    assert bound == "lds" and ops == 2 * (2 * 75 * ((17669 + 31) // 32))  # Encaps + re-encryption
+    kernels, roof, _ = bench.kernel_report("HQC-128", "encdec", {"k_hqc_enc_mul": (0.8, 2)}, 1 << 16)
+    k = kernels["k_hqc_enc_mul"]
+    assert k["frac"] == pytest.approx(ops * (1 << 16) / 0.8e-3 / bench.LDS_LOOKUP_PEAK)
+    assert k["valu_frac"] == pytest.approx(k["frac"] * 2 * bench.LDS_LOOKUP_PEAK / bench.VALU_PEAK)
+    assert roof["bound"] == "lds" and roof["valu_frac"] == pytest.approx(k["valu_frac"])
