@@ -37,6 +37,45 @@ __device__ __forceinline__ uint32_t ld_byte(const uint8_t* p, size_t i, size_t l
 
 // 12 input bytes -> 16 characters; `have` = bytes present (1..12); missing groups / bytes give
 // '=' padding (RFC 4648: 1 byte -> xx==, 2 bytes -> xxx=).
+__device__ __forceinline__ void encode_chunk(const uint32_t (&w)[3], uint32_t have, const char* tb, uint32_t tl,
+                                             uint8_t* dst) {
+  uint32_t o[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    // bytes 3g .. 3g+2 of the chunk as a big-endian 24-bit value
+    const int b = 3 * g;
+    const uint32_t b0 = (w[b >> 2] >> (8 * (b & 3))) & 0xFF;
+    const uint32_t b1 = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xFF;
+    const uint32_t b2 = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xFF;
+    const uint32_t x = b0 << 16 | b1 << 8 | b2;
+    const uint32_t c0 = *(const uint32_t*)(tb + (((x >> 11) & 0x1F80u) | tl));
+    const uint32_t c1 = *(const uint32_t*)(tb + (((x >> 5) & 0x1F80u) | tl));
+    const uint32_t c2 = *(const uint32_t*)(tb + (((x << 1) & 0x1F80u) | tl));
+    const uint32_t c3 = *(const uint32_t*)(tb + (((x << 7) & 0x1F80u) | tl));
+    uint32_t v = c0 | c1 << 8 | c2 << 16 | c3 << 24;
+    const int rem = (int)have - b;  // bytes of this group present
+    if (rem <= 0) v = 0;            // beyond the record: not stored
+    else if (rem == 1) v = (v & 0xFFFFu) | 0x3D3D0000u;
+    else if (rem == 2) v = (v & 0xFFFFFFu) | 0x3D000000u;
+    o[g] = v;
+  }
+  const uint32_t ngroups = (have + 2) / 3;
+  if (ngroups == 4 && ((uintptr_t)dst & 3) == 0) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) ((uint32_t*)dst)[g] = o[g];
+  } else {
+    for (uint32_t g = 0; g < ngroups; ++g)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dst[4 * g + k] = (uint8_t)(o[g] >> (8 * k));
+  }
+}
+
+// Each lane takes ENC_U chunks of the grid-stride walk per iteration and issues all their loads
+// before the first use: HBM-bound, the kernel needs bytes in flight, and one 12-byte load per
+// lane at a time (rounds 2-4) held 0.42 of the 8 TB/s peak.  Same box, three interleaved rounds
+// (profiles/r5/wire/): the wire step 2.61e8 -> 3.19e8 exchanges/s at 4 in flight, 2 the same,
+// 8 slower (66 / 93 VGPRs for encode / decode: fewer waves).
+constexpr int ENC_U = 4;
 __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __restrict__ in, uint32_t L,
                                                     uint8_t* __restrict__ out, uint32_t OL) {
   __shared__ uint32_t tab[64 * 32];
@@ -52,47 +91,44 @@ __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __r
   const size_t srec = S / cpr;
   const uint32_t sc = (uint32_t)(S % cpr);
 #pragma unroll 1
-  for (; rec < n; rec += srec, c += sc, (c >= cpr ? (c -= cpr, ++rec) : 0)) {
-    const uint8_t* src = in + rec * L + 12 * c;
-    const uint32_t have = L - 12 * c < 12 ? L - 12 * c : 12;
-    uint32_t w[3];
-    if (have == 12 && ((uintptr_t)src & 3) == 0) {
-      w[0] = ((const uint32_t*)src)[0], w[1] = ((const uint32_t*)src)[1], w[2] = ((const uint32_t*)src)[2];
-    } else {
+  while (rec < n) {
+    size_t r[ENC_U];
+    uint32_t ch[ENC_U], w[ENC_U][3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
-        w[k] = ld_byte(src, 4 * k, have) | ld_byte(src, 4 * k + 1, have) << 8 | ld_byte(src, 4 * k + 2, have) << 16 |
-               ld_byte(src, 4 * k + 3, have) << 24;
+    for (int u = 0; u < ENC_U; ++u) {
+      r[u] = rec;
+      ch[u] = c;
+      rec += srec, c += sc;
+      if (c >= cpr) c -= cpr, ++rec;
     }
-    uint32_t o[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      // bytes 3g .. 3g+2 of the chunk as a big-endian 24-bit value
-      const int b = 3 * g;
-      const uint32_t b0 = (w[b >> 2] >> (8 * (b & 3))) & 0xFF;
-      const uint32_t b1 = (w[(b + 1) >> 2] >> (8 * ((b + 1) & 3))) & 0xFF;
-      const uint32_t b2 = (w[(b + 2) >> 2] >> (8 * ((b + 2) & 3))) & 0xFF;
-      const uint32_t x = b0 << 16 | b1 << 8 | b2;
-      const uint32_t c0 = *(const uint32_t*)(tb + (((x >> 11) & 0x1F80u) | tl));
-      const uint32_t c1 = *(const uint32_t*)(tb + (((x >> 5) & 0x1F80u) | tl));
-      const uint32_t c2 = *(const uint32_t*)(tb + (((x << 1) & 0x1F80u) | tl));
-      const uint32_t c3 = *(const uint32_t*)(tb + (((x << 7) & 0x1F80u) | tl));
-      uint32_t v = c0 | c1 << 8 | c2 << 16 | c3 << 24;
-      const int rem = (int)have - b;  // bytes of this group present
-      if (rem <= 0) v = 0;            // beyond the record: not stored
-      else if (rem == 1) v = (v & 0xFFFFu) | 0x3D3D0000u;
-      else if (rem == 2) v = (v & 0xFFFFFFu) | 0x3D000000u;
-      o[g] = v;
+    for (int u = 0; u < ENC_U; ++u) {
+      const uint8_t* src = in + r[u] * L + 12 * ch[u];
+      const uint32_t have = L - 12 * ch[u] < 12 ? L - 12 * ch[u] : 12;
+      if (r[u] >= n) {
+        w[u][0] = w[u][1] = w[u][2] = 0u;
+      } else if (((uintptr_t)src & 3) == 0 && (have == 12 || r[u] + 1 < n)) {
+        // a record's short last chunk reads into the next record (the same buffer) and masks those
+        // bytes off, so the wave never takes the byte-wise path for it
+        const uint3 v = *(const uint3*)src;
+        w[u][0] = v.x, w[u][1] = v.y, w[u][2] = v.z;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int keep = (int)have - 4 * k;  // bytes of word k inside the record
+          w[u][k] &= keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          w[u][k] = ld_byte(src, 4 * k, have) | ld_byte(src, 4 * k + 1, have) << 8 |
+                    ld_byte(src, 4 * k + 2, have) << 16 | ld_byte(src, 4 * k + 3, have) << 24;
+      }
     }
-    uint8_t* dst = out + rec * OL + 16 * c;
-    const uint32_t ngroups = (have + 2) / 3;
-    if (ngroups == 4 && ((uintptr_t)dst & 3) == 0) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) ((uint32_t*)dst)[g] = o[g];
-    } else {
-      for (uint32_t g = 0; g < ngroups; ++g)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dst[4 * g + k] = (uint8_t)(o[g] >> (8 * k));
+    for (int u = 0; u < ENC_U; ++u) {
+      if (r[u] >= n) break;  // the walk is monotonic: the later slots are past the end too
+      const uint32_t have = L - 12 * ch[u] < 12 ? L - 12 * ch[u] : 12;
+      encode_chunk(w[u], have, tb, tl, out + r[u] * OL + 16 * ch[u]);
     }
   }
 }
@@ -100,6 +136,8 @@ __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __r
 // 16 characters -> 12 bytes (fewer in the record's last chunk).  Strict: a character outside
 // the alphabet, '=' anywhere but the final 1-2 padding positions, or a padding count that does
 // not match the output length marks the record invalid (status -1); the caller zeroes status.
+// Loads of DEC_U chunks per lane in flight before the first use, as in the encoder.
+constexpr int DEC_U = 4;
 __global__ __launch_bounds__(256) void k_b64_decode(size_t n, const uint8_t* __restrict__ in, uint32_t IL,
                                                     uint8_t* __restrict__ out, uint32_t L,
                                                     int32_t* __restrict__ status) {
@@ -117,56 +155,77 @@ __global__ __launch_bounds__(256) void k_b64_decode(size_t n, const uint8_t* __r
   const size_t srec = S / cpr;
   const uint32_t sc = (uint32_t)(S % cpr);
 #pragma unroll 1
-  for (; rec < n; rec += srec, c += sc, (c >= cpr ? (c -= cpr, ++rec) : 0)) {
-    const uint8_t* src = in + rec * IL + 16 * c;
-    const uint32_t nch = IL - 16 * c < 16 ? IL - 16 * c : 16;  // a multiple of 4
-    uint32_t w[4];
-    if (nch == 16 && ((uintptr_t)src & 3) == 0) {
+  while (rec < n) {
+    size_t r[DEC_U];
+    uint32_t chs[DEC_U], w[DEC_U][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) w[k] = ((const uint32_t*)src)[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        w[k] = 4 * k < (int)nch ? (uint32_t)src[4 * k] | (uint32_t)src[4 * k + 1] << 8 |
-                                      (uint32_t)src[4 * k + 2] << 16 | (uint32_t)src[4 * k + 3] << 24
-                                : 0u;
+    for (int u = 0; u < DEC_U; ++u) {
+      r[u] = rec;
+      chs[u] = c;
+      rec += srec, c += sc;
+      if (c >= cpr) c -= cpr, ++rec;
     }
-    const uint32_t last_chunk = c + 1 == cpr;
-    const uint32_t have = last_chunk ? have_last : 12;  // output bytes of this chunk
-    uint32_t bad = 0, o[3] = {0, 0, 0};
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (4 * g >= (int)nch) break;
-      uint32_t v = 0;
+    for (int u = 0; u < DEC_U; ++u) {
+      const uint8_t* src = in + r[u] * IL + 16 * chs[u];
+      const uint32_t nch = IL - 16 * chs[u] < 16 ? IL - 16 * chs[u] : 16;  // a multiple of 4
+      if (r[u] >= n) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t ch = (w[g] >> (8 * k)) & 0xFF;
-        uint32_t d = *(const uint32_t*)(tb + (((ch << 7) & 0x3F80u) | tl)) | (ch & 0x80u);
-        // padding is legal only in the last group of the record, last `pad` positions
-        const bool is_pad_pos = last_chunk && 4 * g + 4 == (int)nch && k >= 4 - (int)pad;
-        if (is_pad_pos) {
-          bad |= ch != '=';
-          d = 0;
-        } else {
-          bad |= d >> 6;
+        for (int k = 0; k < 4; ++k) w[u][k] = 0u;
+      } else if (((uintptr_t)src & 3) == 0 && (nch == 16 || r[u] + 1 < n)) {
+        // a record's short last chunk reads into the next record; words past nch are never used
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[u][k] = ((const uint32_t*)src)[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          w[u][k] = 4 * k < (int)nch ? (uint32_t)src[4 * k] | (uint32_t)src[4 * k + 1] << 8 |
+                                          (uint32_t)src[4 * k + 2] << 16 | (uint32_t)src[4 * k + 3] << 24
+                                    : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DEC_U; ++u) {
+      if (r[u] >= n) break;  // the walk is monotonic
+      const uint32_t cc = chs[u];
+      const uint32_t nch = IL - 16 * cc < 16 ? IL - 16 * cc : 16;
+      const uint32_t last_chunk = cc + 1 == cpr;
+      const uint32_t have = last_chunk ? have_last : 12;  // output bytes of this chunk
+      uint32_t bad = 0, o[3] = {0, 0, 0};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (4 * g >= (int)nch) break;
+        uint32_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t ch = (w[u][g] >> (8 * k)) & 0xFF;
+          uint32_t d = *(const uint32_t*)(tb + (((ch << 7) & 0x3F80u) | tl)) | (ch & 0x80u);
+          // padding is legal only in the last group of the record, last `pad` positions
+          const bool is_pad_pos = last_chunk && 4 * g + 4 == (int)nch && k >= 4 - (int)pad;
+          if (is_pad_pos) {
+            bad |= ch != '=';
+            d = 0;
+          } else {
+            bad |= d >> 6;
+          }
+          v = v << 6 | (d & 63);
         }
-        v = v << 6 | (d & 63);
-      }
-      // v = 24-bit big-endian group -> bytes 3g .. 3g+2 of the chunk
+        // v = 24-bit big-endian group -> bytes 3g .. 3g+2 of the chunk
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int b = 3 * g + k;
-        o[b >> 2] |= ((v >> (16 - 8 * k)) & 0xFF) << (8 * (b & 3));
+        for (int k = 0; k < 3; ++k) {
+          const int b = 3 * g + k;
+          o[b >> 2] |= ((v >> (16 - 8 * k)) & 0xFF) << (8 * (b & 3));
+        }
       }
-    }
-    uint8_t* dst = out + rec * L + 12 * c;
-    if (have == 12 && ((uintptr_t)dst & 3) == 0) {
+      uint8_t* dst = out + r[u] * L + 12 * cc;
+      if (have == 12 && ((uintptr_t)dst & 3) == 0) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ((uint32_t*)dst)[k] = o[k];
-    } else {
-      for (uint32_t b = 0; b < have; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+        for (int k = 0; k < 3; ++k) ((uint32_t*)dst)[k] = o[k];
+      } else {
+        for (uint32_t b = 0; b < have; ++b) dst[b] = (uint8_t)(o[b >> 2] >> (8 * (b & 3)));
+      }
+      if (bad && status) status[r[u]] = -1;
     }
-    if (bad && status) status[rec] = -1;
   }
 }
 
