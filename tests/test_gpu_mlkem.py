@@ -318,7 +318,8 @@ def test_sample_ntt_fixup_resume_and_overflow(engines, alg, k, n):
     assert np.array_equal(_host(ss)[idx], oss)
 
 
-def test_fixup_counters_across_calls():
+@pytest.mark.parametrize("alg,k", [("ML-KEM-512", 2), ("ML-KEM-768", 3), ("ML-KEM-1024", 4)])
+def test_fixup_counters_across_calls(alg, k):
     """Chunks of at most 2^15 read rho from the keys and count SampleNTT fix-ups into one of the
     context's two counters, each call zeroing the other for the next (no k_rho_copy launch).  A run of
     Encaps / Decaps calls whose every pk needs fix-ups -- direct-path chunks back to back, a call split
@@ -326,8 +327,7 @@ def test_fixup_counters_across_calls():
     oracle on every call (Decaps with dk's copy of rho replaced too)."""
     import oracle as orc
     from qrkem.batch import BatchKEM
-    alg, k = "ML-KEM-768", 3
-    rng = np.random.default_rng(91)
+    rng = np.random.default_rng(91 + k)
     for _ in range(4000):
         rho = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
         if sum(_sample_ntt_needs_4th_block(rho, i, j) for i in range(k) for j in range(k)) >= 1:
