@@ -156,6 +156,11 @@ struct qrk_ctx {
   uint32_t* hflag = nullptr;      // single-shot completion flag (fine-grained pinned) ...
   uint32_t* hflag_dev = nullptr;  // ... its device address
   uint32_t* kg_cnt = nullptr;     // multi-workgroup ML-KEM KeyGen arrival counters (zeroed at allocation)
+  bool kg_dirty = false;          // a pipelined KeyGen failed: a straggler may have set a flag word
+                                  // after the collector's reset, or stored scratch after its wipe
+  bool kg_err_next = false;       // run_batch: hand the KeyGen error word (hflag[1]) to the next launch
+  uint64_t* xof_keep_next = nullptr;        // run_batch: Streams::xof_keep / xof_given of the next
+  const uint64_t* xof_given_next = nullptr;  // call (handshake driver, one chunk)
   uint32_t* fixc = nullptr;       // ML-KEM SampleNTT fix-up counters of chunks <= 2^15 (Streams::fixc)
   int fixp = 0;                   // the counter the next such chunk counts into
   bool fixc_dirty = false;        // a chunk's launches failed after the parity flip: re-zero both
@@ -389,7 +394,19 @@ static int run_batch(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8_t* o
       if (e == hipSuccess) e = hipMemset(ctx->kg_cnt, 0, mlkem_kg_flag_words() * sizeof(uint32_t));
       if (e != hipSuccess) return hip_fail("hipMalloc(kg_cnt)", e);
     }
+    if (ctx->kg_dirty) {  // stream-ordered behind the failed call's kernel
+      hipError_t e = hipMemsetAsync(ctx->kg_cnt, 0, mlkem_kg_flag_words() * sizeof(uint32_t), st);
+      if (e == hipSuccess && ctx->scratch)
+        e = hipMemsetAsync(ctx->scratch, 0, std::min(ctx->scratch_bytes, mlkem_kg_scratch_bytes()), st);
+      if (e != hipSuccess) return hip_fail("hipMemsetAsync(kg_cnt)", e);
+      ctx->kg_dirty = false;
+    }
     S.kg_cnt = ctx->kg_cnt;
+    if (ctx->kg_err_next) S.kg_err = ctx->hflag_dev + 1;
+  }
+  if (a.family == Family::MLKEM && n <= chunk && n > mlkem_small_max()) {
+    S.xof_keep = op == Op::KEYPAIR ? ctx->xof_keep_next : nullptr;
+    S.xof_given = op == Op::DECAPS ? ctx->xof_given_next : nullptr;
   }
   if (a.family == Family::MLKEM && op != Op::KEYPAIR) {
     if (!ctx->fixc) {
@@ -526,6 +543,12 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   // n == 1: the kernel stores a ticket in fine-grained pinned memory once its outputs are visible,
   // and the host spins on it (about 4 us sooner than hipStreamSynchronize wakes up)
   const bool spin = n == 1 && flag_ready(ctx) == 0;
+  // ML-KEM KeyGen: the pipelined kernel's error word, hflag[1] (the flag's 64-byte line)
+  const bool kg_err = op == Op::KEYPAIR && n <= mlkem_kg_multi_max() && flag_ready(ctx) == 0;
+  if (kg_err) {
+    __atomic_store_n(ctx->hflag + 1, 0u, __ATOMIC_RELEASE);
+    ctx->kg_err_next = true;
+  }
   if (spin) {
     ctx->ticket = ctx->ticket + 1 ? ctx->ticket + 1 : 1;
     ctx->flag_next = true;
@@ -538,6 +561,7 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
   HT(5);
   ctx->flag_next = false;
   ctx->hin_next = nullptr;
+  ctx->kg_err_next = false;
   hipError_t e = hipSuccess;
   if (!rc && spin) {
     // bounded spin; a kernel that never stores the ticket (a launch or execution error) falls
@@ -557,12 +581,26 @@ static int run_small_host(qrk_ctx* ctx, const AlgInfo& a, Op op, size_t n, uint8
     e = hipStreamSynchronize(st);
   }
   if (!rc && e != hipSuccess) rc = hip_fail("kernel execution", e);
+  // the collector stores the error word before the ticket (or the kernel's end, which the stream
+  // synchronise waited for)
+  if (!rc && kg_err && __atomic_load_n(ctx->hflag + 1, __ATOMIC_ACQUIRE) != 0)
+    rc = fail("ML-KEM KeyGen: keygen hand-off timeout (a bounded cross-workgroup wait expired)");
+  if (rc && kg_err) ctx->kg_dirty = true;  // re-zeroed (flags, scratch) before the next KeyGen launch
   if (!rc) {
     memcpy(o1, h + o_o1, n * l_o1);
     if (l_o2) memcpy(o2, h + o_o2, n * l_o2);
     if (status) memcpy(status, h + o_st, n * sizeof(int32_t));
   }
   if (rc) (void)hipStreamSynchronize(st);  // nothing may still read or write the mirror
+  if (rc && ctx->kg_dirty && ctx->kg_cnt) {
+    // wipe the secret scratch a straggler may have written after the collector's wipe now, not at
+    // the next KeyGen (run_batch re-zeroes again if this fails)
+    hipError_t w = hipMemsetAsync(ctx->kg_cnt, 0, mlkem_kg_flag_words() * sizeof(uint32_t), st);
+    if (w == hipSuccess && ctx->scratch)
+      w = hipMemsetAsync(ctx->scratch, 0, std::min(ctx->scratch_bytes, mlkem_kg_scratch_bytes()), st);
+    if (w == hipSuccess) w = hipStreamSynchronize(st);
+    if (w == hipSuccess) ctx->kg_dirty = false;
+  }
   OQS_MEM_cleanse(h, total);  // coins, secret keys and shared secrets do not outlive the call
   HT(7);
   return rc;
@@ -885,6 +923,13 @@ int qrk_ctx_staging_residue(qrk_ctx* ctx, uint64_t out[3]) {
   return 0;
 }
 
+// Tests only (not in qrkem.h): PRF item `item` of the pipelined single-shot ML-KEM KeyGen publishes
+// its payload and flags 150 ms late, past every bounded wait (-1: off).  Process-wide.
+extern "C" int qrk_dbg_kg_late(int item) {
+  g_kg_dbg_late = item;
+  return 0;
+}
+
 // Tests only (not in qrkem.h): nonzero bytes left in the ML-KEM per-handshake records of a chunk
 // of n handshakes (mlkem_cleanse wipes them after every chunk).
 extern "C" int qrk_dbg_mlkem_records_residue(qrk_ctx* ctx, const char* alg, size_t n, uint64_t* out) {
@@ -1082,8 +1127,18 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
   const size_t m0 = std::min(chunk, n);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t b_sk = al(m0 * a->sk), b_ss = al(m0 * a->ss);
-  if (grow_device(ctx, (void**)&ctx->hs_scratch, &ctx->hs_scratch_bytes, 2 * b_sk + 2 * b_ss, st)) return -1;
+  // ML-KEM batched chunks: the initiator's sampled matrix A_hat, kept from its KeyGen (:590) for its
+  // Decaps (:1038) -- the same rho, so Decaps skips K^2 SampleNTT entries (27 of a handshake's ~174
+  // ML-KEM-768 permutations).  Public data (a function of rho): outside the wiped range.
+  const bool keep_a = a->family == Family::MLKEM && m0 > mlkem_small_max();
+  const size_t b_mat = keep_a ? al(mlkem_matrix_bytes(*a, m0)) : 0;
+  if (grow_device(ctx, (void**)&ctx->hs_scratch, &ctx->hs_scratch_bytes, 2 * b_sk + 2 * b_ss + b_mat, st)) return -1;
   uint8_t *sk_i = ctx->hs_scratch, *sk_r = sk_i + b_sk, *ss_i = sk_r + b_sk, *ss_r = ss_i + b_ss;
+  uint64_t* mat_i = keep_a ? (uint64_t*)(ss_r + b_ss) : nullptr;
+  struct NextReset {  // the hand-over fields never outlive one run_batch call
+    qrk_ctx* c;
+    ~NextReset() { c->xof_keep_next = nullptr, c->xof_given_next = nullptr; }
+  } next_reset{ctx};
   // wipes the ephemeral sk / ss on every exit path, error returns included (runs before
   // last_use records the end of the call)
   struct Wipe {
@@ -1095,10 +1150,13 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
   for (size_t off = 0; off < n; off += chunk) {
     const size_t m = std::min(chunk, n - off);
     auto co = [&](const uint8_t* c, size_t len) { return c ? c + off * len : nullptr; };
-    // initiate_key_exchange: ephemeral KeyGen (messaging.py:590)
-    if (run_batch(ctx, *a, Op::KEYPAIR, m, pk_i + off * a->pk, sk_i, co(coins_kp_i, a->kp_coins), nullptr, nullptr,
-                  st))
-      return -1;
+    // initiate_key_exchange: ephemeral KeyGen (messaging.py:590); A_hat kept for its Decaps
+    const bool keep = keep_a && m > mlkem_small_max();
+    ctx->xof_keep_next = keep ? mat_i : nullptr;
+    const int rc_kg = run_batch(ctx, *a, Op::KEYPAIR, m, pk_i + off * a->pk, sk_i, co(coins_kp_i, a->kp_coins), nullptr,
+                                nullptr, st);
+    ctx->xof_keep_next = nullptr;
+    if (rc_kg) return -1;
     // _handle_key_exchange_init: responder KeyGen (:809, pk sent back at :853) + Encaps (:830)
     if (run_batch(ctx, *a, Op::KEYPAIR, m, pk_r + off * a->pk, sk_r, co(coins_kp_r, a->kp_coins), nullptr, nullptr,
                   st))
@@ -1110,7 +1168,10 @@ int qrk_handshake_batch(qrk_ctx* ctx, const char* alg, size_t n, const uint8_t* 
                                info_len, key_len, key_r + off * key_len, key_len, st);  // :845
     if (e != hipSuccess) return hip_fail("hkdf_sha256", e);
     // _handle_key_exchange_response: Decaps (:1038) + HKDF (:1068)
-    if (run_batch(ctx, *a, Op::DECAPS, m, ss_i, nullptr, ct + off * a->ct, sk_i, nullptr, st)) return -1;
+    ctx->xof_given_next = keep ? mat_i : nullptr;
+    const int rc_dec = run_batch(ctx, *a, Op::DECAPS, m, ss_i, nullptr, ct + off * a->ct, sk_i, nullptr, st);
+    ctx->xof_given_next = nullptr;
+    if (rc_dec) return -1;
     e = hkdf_sha256(m, ss_i, a->ss, a->ss, nullptr, 0, info, info_off ? info_off + off : nullptr, info_len,
                     key_len, key_i + off * key_len, key_len, st);
     if (e != hipSuccess) return hip_fail("hkdf_sha256", e);

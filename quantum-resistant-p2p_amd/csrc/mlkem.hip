@@ -1917,12 +1917,13 @@ __global__ __launch_bounds__(64 * KG_WAVES) void k_keygen_one(size_t n, const ui
 #ifndef QRK_KG_MULTI_MAX
 #define QRK_KG_MULTI_MAX 16
 #endif
-// 1: k_keygen_pipe (H(ek) pipelined with SampleNTT, below; measured 37.5 against 41.6 us per kernel,
-// profiles/r5/single_shot/); 0 (default): k_keygen_multi.  The pipelined kernel stays opt-in
-// (tools/build_variant.sh ... -DQRK_KG_PIPE=1) until its completion / key-wipe ordering has been
-// reviewed.
+// 1 (default): host-pointer KeyGen calls of n <= QRK_KG_MULTI_MAX run k_keygen_pipe (H(ek) pipelined
+// with SampleNTT, below; 37.5 against 41.6 us per kernel, profiles/r5/single_shot/), which reports a
+// lost hand-off through the call's error word (Streams::kg_err); device-pointer calls, which have no
+// host-visible error word, keep k_keygen_multi (no cross-workgroup waits, so nothing to time out).
+// 0: k_keygen_multi everywhere (A/B builds: tools/build_variant.sh ... -DQRK_KG_PIPE=0).
 #ifndef QRK_KG_PIPE
-#define QRK_KG_PIPE 0
+#define QRK_KG_PIPE 1
 #endif
 struct MkScr {
   uint4 xs[32 * 16];        // SampleNTT entries, load_sampled<16> layout (K^2 <= 16)
@@ -1943,11 +1944,8 @@ __device__ __forceinline__ void mk_wipe_lds(MkLds& sl) {
   for (int x = threadIdx.x; x < (int)(sizeof(MkLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
 }
 
-struct KgCoins {  // one handshake's KeyGen coins d || z passed by value (single-shot host calls)
-  uint64_t w[8];
-};
 template <int K>
-__global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __restrict__ coins, KgCoins cv,
+__global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __restrict__ coins,
                                                      uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
                                                      MkScr* __restrict__ scr_all, uint32_t* __restrict__ cnt,
                                                      uint32_t* done, uint32_t ticket) {
@@ -1961,9 +1959,9 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
   MkScr& scr = scr_all[hs];
   uint8_t* ek = pk + hs * P<K>::PK;
   uint8_t* dk = sk + hs * P<K>::SK;
-  // the coins row: the kernel argument (n == 1 host calls: no PCIe read before G) or memory; z for
-  // dk's tail is loaded with d rather than after H(ek) in the last workgroup
-  const uint64_t* cw = coins ? (const uint64_t*)(coins + hs * 64) : cv.w;
+  // the coins row (secret: always memory, never a kernel argument); z for dk's tail is loaded with d
+  // rather than after H(ek) in the last workgroup
+  const uint64_t* cw = (const uint64_t*)(coins + hs * 64);
   const uint64_t zw = (i >= 0 && i < 4) ? cw[4 + i] : 0;
   SS_MARK(blockIdx.x == 0 && lane == 0, 0);
   SS_MARK(blockIdx.x == NI - 1 && lane == 0, 14);
@@ -2097,11 +2095,20 @@ __global__ __launch_bounds__(64) void k_keygen_multi(size_t n, const uint8_t* __
 //     then copies t_hat_1 .. t_hat_{K-1} in from the row workgroups; wave K + 1 computes G itself
 //     and absorbs ek block by block as its bytes arrive
 // The critical path becomes G, SampleNTT's first two blocks (one block yields ~91 coefficients,
-// H's block 0 needs 92), then the nine H(ek) permutations: 11 permutations.  Every consumer polls
-// one flag word with relaxed sc1 loads (bounded spin) and loads the payload with sc1 loads only.
-// The collector waits until every other workgroup has published its host outputs (system-scope
-// release before the flag when the outputs are host memory), wipes the secret scratch (s_hat,
-// e_hat), resets the flags and stores the completion ticket.
+// H's block 0 needs 92), then the nine H(ek) permutations: 11 permutations.
+// Hand-offs (MI355X_MICROARCH.md "Valid forms", the Consumer bullet with the acquire kept): the
+// producer wave stores every payload byte with sc1 stores, waits vmcnt(0), then one lane stores the
+// flag (sc1); the consumer wave polls the flag with relaxed sc1 loads, then ONE agent-scope acquire
+// (buffer_inv sc1 + vmcnt(0): the CU's L1 may hold a stale line, the producer may sit on another
+// XCD), then loads the payload in that same wave.
+// Failure semantics: every wait is a bounded spin (KG_SPIN_TICKS).  A wait that expires marks its
+// workgroup in error; a workgroup's outputs-done flag carries it (2 instead of 1); the collector,
+// which waits for every other workgroup's flag, stores 1 into the call's error word (host-mapped,
+// Streams::kg_err) before the completion ticket when any wait of the handshake expired, and the host
+// returns OQS_ERROR for the call, re-zeroes the flag words (a straggler may set one after the
+// collector's reset) and wipes the scratch.  The collector waits until every other workgroup has
+// published its host outputs (system-scope release before the flag when the outputs are host
+// memory), wipes the secret scratch (s_hat, e_hat), resets the flags and stores the ticket.
 struct PipeScr {
   uint32_t bop[4][16][16];  // NTT(s_j) basemul operands, word w of lane L at [j][w][L] (secret)
   float ef[4][16][16];      // NTT(e_i), coefficient t of lane L at [i][t][L] (secret)
@@ -2121,6 +2128,7 @@ struct PipeLds {
   uint64_t sigma[4];
   GroupLds g;
   int prog[4], io_ready;
+  int err;  // a bounded wait of this workgroup expired
 };
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint64_t gu64;
@@ -2130,40 +2138,59 @@ __device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
   return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// bounded spins (50 ms of the 100 MHz wall clock): a lost hand-off ends the kernel with wrong
-// outputs instead of hanging the GPU
+// bounded spins (50 ms of the 100 MHz wall clock): a lost hand-off ends the kernel (and reports
+// itself through the error word) instead of hanging the GPU
 constexpr uint64_t KG_SPIN_TICKS = 5000000;
-// one wave polls flag words (relaxed sc1 loads, all of them issued per pass); its payload loads
-// after this are sc1 loads only
-template <int NF>
-__device__ __forceinline__ void kg_wait_flags(const uint32_t* const (&f)[NF]) {
+// one wave polls flag words (relaxed sc1 loads, all of them issued per pass) until every one is
+// nonzero or the spin expires (returns false); *orv = OR of the values last read.  ACQ: the payload
+// loads that follow in this wave are ordered by one agent-scope acquire (invalidates this CU's L1;
+// its vmcnt(0) waits for the invalidate); without ACQ no payload is read after the poll.
+template <int NF, bool ACQ>
+__device__ __forceinline__ bool kg_wait_flags(const uint32_t* const (&f)[NF], uint32_t* orv = nullptr) {
   const uint64_t t0 = wall_clock64();
-  while (wall_clock64() - t0 < KG_SPIN_TICKS) {
+  bool all;
+  uint32_t o;
+  for (;;) {
     uint32_t v[NF];
 #pragma unroll
     for (int k = 0; k < NF; ++k) v[k] = ld_sc1(f[k]);
-    bool all = true;
+    all = true;
+    o = 0u;
 #pragma unroll
-    for (int k = 0; k < NF; ++k) all = all && v[k] != 0u;
-    if (all) break;
+    for (int k = 0; k < NF; ++k) all = all && v[k] != 0u, o |= v[k];
+    if (all || wall_clock64() - t0 >= KG_SPIN_TICKS) break;
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the payload loads below the poll
+  if (ACQ) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (orv) *orv = o;
+  return all;
 }
-__device__ __forceinline__ void kg_wait_flag(const uint32_t* f) {
+__device__ __forceinline__ bool kg_wait_flag(const uint32_t* f) {
   const uint32_t* const a[1] = {f};
-  kg_wait_flags<1>(a);
+  return kg_wait_flags<1, true>(a);
 }
 // the storing wave's sc1 stores drained, then one lane stores the flag
 __device__ __forceinline__ void kg_publish(uint32_t* f) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if ((threadIdx.x & 63) == 0) st_sc1(f, 1u);
 }
-__device__ __forceinline__ void lds_wait_ge(const int* p, int v) {
+__device__ __forceinline__ bool lds_wait_ge(const int* p, int v) {
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v && wall_clock64() - t0 < KG_SPIN_TICKS)
+  bool ok;
+  while (!(ok = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) &&
+         wall_clock64() - t0 < KG_SPIN_TICKS)
     __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return ok;
+}
+// a wave whose bounded wait expired marks its workgroup in error (the whole wave stores the same 1)
+__device__ __forceinline__ void kg_mark(PipeLds& sl, bool ok) {
+  if (!ok) sl.err = 1;
 }
 __device__ __forceinline__ void lds_release_store(int* p, int v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -2201,7 +2228,7 @@ __device__ __forceinline__ void kg_load_ops(PipeLds& sl, const PipeScr& scr, con
 #pragma unroll
   for (int j = 0; j < K; ++j) f[j] = &fl[j];
   f[K] = &fl[K + r];
-  kg_wait_flags<K + 1>(f);
+  kg_mark(sl, kg_wait_flags<K + 1, true>(f));
   const int lane = threadIdx.x & 63;
   constexpr int NB = K * 128 / 64, NE = 128 / 64;  // u64 words per lane
   uint64_t vb[NB], ve[NE];
@@ -2233,11 +2260,14 @@ __device__ __forceinline__ uint32_t kg_pipe_pair(const PipeLds& sl, int p, BopAt
   const uint32_t t1 = (uint32_t)canon_f(acc_to_f(a1) + ef_at(2 * u + 1, L));
   return t0 | (t1 << 12);  // 24 bits, little-endian ek bytes 3p .. 3p + 2
 }
+// debug builds of a test: PRF item `late` (>= 0) sleeps this long before it stores its payload and
+// flags, past every consumer's and the collector's bounded wait (qrk_dbg_kg_late, tests only)
+constexpr uint64_t KG_DBG_LATE_TICKS = 15000000;  // 150 ms
 template <int K>
 __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const uint8_t* __restrict__ coins,
                                                               uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
                                                               PipeScr* __restrict__ scr_all, uint32_t* __restrict__ flags,
-                                                              uint32_t* done, uint32_t ticket) {
+                                                              uint32_t* done, uint32_t ticket, uint32_t* err, int late) {
   constexpr int NWG = 3 * K, PKB = P<K>::PK;
   __shared__ __attribute__((aligned(16))) PipeLds sl;
   const size_t hs = blockIdx.x / NWG;
@@ -2250,23 +2280,28 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
   uint8_t* ek = pk + hs * PKB;
   uint8_t* dk = sk + hs * P<K>::SK;
   const uint64_t* d = (const uint64_t*)(coins + hs * 64);
+  // returns whether any wait of this workgroup expired, then wipes the LDS
   auto wipe_lds = [&] {
+    __syncthreads();
+    const int e = sl.err;
     __syncthreads();
     uint4* w = (uint4*)&sl;
     for (int x = threadIdx.x; x < (int)(sizeof(PipeLds) / 16); x += (int)blockDim.x) w[x] = make_uint4(0, 0, 0, 0);
+    return e != 0;
   };
   // a non-collector workgroup's last act (after its LDS wipe): its host-memory outputs released at
-  // system scope, then its flag (the collector's done ticket follows every such flag)
-  auto outputs_done = [&](int w) {
+  // system scope, then its flag, 2 when one of its waits expired (the collector's done ticket follows
+  // every such flag)
+  auto outputs_done = [&](int w, bool e) {
     if (done) __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_sc1(&fl[16 + w], 1u);
+      st_sc1(&fl[16 + w], e ? 2u : 1u);
     }
   };
   if (threadIdx.x < 4) sl.prog[threadIdx.x] = 0;
-  if (threadIdx.x == 0) sl.io_ready = 0;
+  if (threadIdx.x == 0) sl.io_ready = 0, sl.err = 0;
   __syncthreads();
   SS_MARK(role == NWG - 1 && threadIdx.x == 0, 0);
   if (role < 2 * K) {  // ------------------------------------------------ PRF item N = role
@@ -2282,6 +2317,10 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1, 16>(sl.ps, (size_t)N, lane));
         contig_to_stride_f(f, (float*)sl.g.poly, lane);
         ntt_fwd_f<false>(f, (float*)sl.g.poly, lane);
+        if (N == late) {
+          const uint64_t t0 = wall_clock64();
+          while (wall_clock64() - t0 < KG_DBG_LATE_TICKS) __builtin_amdgcn_s_sleep(127);
+        }
         if (N < K) {
           const BOp b = make_bop_f(f, lane);
 #pragma unroll
@@ -2303,8 +2342,9 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         encode12(t, dk + 384 * N, lane);
       }
     }
-    wipe_lds();  // sigma, the PRF output and NTT(s) / NTT(e): wiped before the flag that ends this workgroup
-    outputs_done(N);
+    // sigma, the PRF output and NTT(s) / NTT(e): wiped before the flag that ends this workgroup
+    const bool e = wipe_lds();
+    outputs_done(N, e);
     return;
   }
   const int r = role < NWG - 1 ? role - 2 * K + 1 : 0;  // the matrix row of this workgroup
@@ -2316,7 +2356,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
     if (wave == 0) {
       kg_load_ops<K>(sl, scr, fl, r);
 #pragma unroll
-      for (int j = 0; j < K; ++j) lds_wait_ge(&sl.prog[j], 256);
+      for (int j = 0; j < K; ++j) kg_mark(sl, lds_wait_ge(&sl.prog[j], 256));
       // lane l: pairs l and l + 64
       uint32_t tb[2];
 #pragma unroll
@@ -2343,8 +2383,8 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         ((uint32_t*)(dk + 384 * K + 384 * r))[w] = io32[w];
       }
     }
-    wipe_lds();  // the s_hat / e_hat copies: wiped before the flag that ends this workgroup
-    outputs_done(2 * K + r - 1);
+    const bool e = wipe_lds();  // the s_hat / e_hat copies: wiped before the flag that ends this workgroup
+    outputs_done(2 * K + r - 1, e);
     return;
   }
   // ------------------------------------------------------------------------ the collector (row 0)
@@ -2357,7 +2397,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
 #pragma unroll 1
     for (int b = 0; b < 3; ++b) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) lds_wait_ge(&sl.prog[j], 2 * LIM[b + 1]);
+      for (int j = 0; j < K; ++j) kg_mark(sl, lds_wait_ge(&sl.prog[j], 2 * LIM[b + 1]));
       const int p = LIM[b] + lane;
       if (p < LIM[b + 1]) {
         const uint32_t t = kg_pipe_pair<K>(
@@ -2375,7 +2415,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
       ((uint32_t*)(dk + 384 * K))[w] = io32[w];
     }
     for (int rr = 1; rr < K; ++rr) {
-      kg_wait_flag(&fl[8 + rr]);
+      kg_mark(sl, kg_wait_flag(&fl[8 + rr]));
       const uint64_t* st = (const uint64_t*)&scr.th[rr][0];
       uint64_t v = 0;
       if (lane < 48) v = __hip_atomic_load((const gu64*)(st + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2393,7 +2433,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
 #pragma unroll 1
     for (int b = 0; b < NFULL; ++b) {
       const int need = 8 * RW * (b + 1) < 384 * K ? 8 * RW * (b + 1) : 384 * K;
-      lds_wait_ge(&sl.io_ready, need);
+      kg_mark(sl, lds_wait_ge(&sl.io_ready, need));
       SS_MARK(lane == 0 && b < 4, 8 + (b == 0 ? 0 : b == 1 ? 5 : b == 2 ? 1 : 6));
       if (rl) cs_xor(s, sl.io[b * RW + i]);
       s = kf_coop(s, c);
@@ -2402,7 +2442,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
     // of G's output: wave 0 wrote it before its first progress release, which the t_hat wave acquired
     // before it released io_ready (this wave computes no G of its own: one cooperative permutation
     // fewer beside the SampleNTT waves)
-    lds_wait_ge(&sl.io_ready, 384 * K);
+    kg_mark(sl, lds_wait_ge(&sl.io_ready, 384 * K));
     if (i >= 0 && i < 4 && coop_canon(c)) {
       const uint64_t rw = sl.rho[0][i];
       sl.io[48 * K + i] = rw;
@@ -2425,20 +2465,24 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
   // Completion, in key-hygiene order: this workgroup's outputs released; its LDS (which holds copies
   // of s_hat and e_hat_0) wiped; every other workgroup's outputs (and its last scratch / flag
   // access) done; the secret scratch (s_hat, e_hat) wiped and the flags reset; those stores drained;
-  // and only then the completion ticket stored for the host -- the ticket is the kernel's last act.
+  // the error word set if any wait of this handshake expired; and only then the completion ticket
+  // stored for the host -- the ticket is the kernel's last act.
   if (done) __threadfence_system();
-  wipe_lds();
+  const bool own_err = wipe_lds();
   __syncthreads();
   if (wave == 0) {
     const uint32_t* of[NWG - 1];
 #pragma unroll
     for (int w = 0; w < NWG - 1; ++w) of[w] = &fl[16 + w];
-    kg_wait_flags<NWG - 1>(of);
+    uint32_t seen = 0u;
+    const bool all = kg_wait_flags<NWG - 1, false>(of, &seen);  // no payload read after it
     uint4* sw = (uint4*)&scr;
     for (int x = lane; x < (int)(offsetof(PipeScr, th) / 16); x += 64) sw[x] = make_uint4(0, 0, 0, 0);
     if (lane < KG_FLAGS) st_sc1(&fl[lane], 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     SS_MARK(lane == 0, 6);
+    if (lane == 0 && (own_err || !all || (seen & 2u)))
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (done && lane == 0) __hip_atomic_store(done, ticket, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -2748,14 +2792,15 @@ template <int K>
 hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins, void* scratch, const Streams& s) {
   const size_t C = round64(n);
   ScratchView v = carve(scratch, K, C);
-  if (QRK_KG_PIPE && n <= QRK_KG_MULTI_MAX && s.kg_cnt) {
+  if (QRK_KG_PIPE && n <= QRK_KG_MULTI_MAX && s.kg_cnt && s.kg_err) {  // host-pointer calls
     QRK_LAUNCH("k_keygen_pipe", s.main, k_keygen_pipe<K>, dim3((unsigned)(n * 3 * K)), dim3(64 * (K + 2)), 0, s.main, n,
-               coins, pk, sk, (PipeScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
+               coins, pk, sk, (PipeScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket, s.kg_err,
+               g_kg_dbg_late);
     return hipGetLastError();
   }
-  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {  // the default (QRK_KG_PIPE=0): the round-4 kernel
+  if (n <= QRK_KG_MULTI_MAX && s.kg_cnt) {  // device-pointer calls (no error word), QRK_KG_PIPE=0 builds
     QRK_LAUNCH("k_keygen_multi", s.main, k_keygen_multi<K>, dim3((unsigned)(n * (2 * K + K * K))), dim3(64), 0,
-               s.main, n, coins, KgCoins{}, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
+               s.main, n, coins, pk, sk, (MkScr*)scratch, s.kg_cnt, n == 1 ? s.done : nullptr, s.ticket);
     return hipGetLastError();
   }
   if (n <= QRK_SMALL_MAX) {
@@ -2764,6 +2809,7 @@ hipError_t keygen_impl(size_t n, uint8_t* pk, uint8_t* sk, const uint8_t* coins,
     return hipGetLastError();
   }
   hipStream_t st = s.main;
+  if (s.xof_keep) v.xof = s.xof_keep;  // the handshake driver keeps A_hat for the same party's Decaps
   QRK_LAUNCH("k_front_keygen", st, k_front_keygen<K>, dim3(blocks_for(n)), dim3(256), 0, st, coins, n, pk, sk,
              v.seeds, v.rho, v.nfix);
   const uint8_t* rho = (const uint8_t*)v.rho;
@@ -2824,12 +2870,24 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   }
   hipStream_t st = s.main;
   const unsigned gblocks = (unsigned)((n + GROUPS - 1) / GROUPS);
-  poison_xof<K>(C, v, st);
-  const RhoSrc rho = rho_source(sk + 768 * K, (size_t)P<K>::SK, n, C, v, s);
   const RDecrypt<K> dec{n, ct, sk, v.mprime, gblocks};
   const RJDec<K> jd{ct, sk, n, v.kbar, blocks_for(n)};
   const RGDec<K> gd{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
+  if (s.xof_given) {  // A_hat from this party's KeyGen (handshake driver): no SampleNTT, no fix-up
+    const RCore<K, 1> core{n, C, s.xof_given, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime,
+                           (size_t)32, const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
+    launch_multi("k_j_decaps+k_decrypt_core", {"k_j_decaps", "k_decrypt_core"}, s, jd, dec);
+    if (C <= QRK_PAIR_FRONT_MAX)
+      launch_one("k_g_decaps", RGDecPair<K>{sk, v.mprime, n, v.seeds, v.kprime, blocks_for(2 * n)}, s);
+    else
+      launch_one("k_g_decaps", gd, s);
+    launch_one("k_prf", prf, s);
+    launch_one("k_encrypt_core", core, s);
+    return hipGetLastError();
+  }
+  poison_xof<K>(C, v, st);
+  const RhoSrc rho = rho_source(sk + 768 * K, (size_t)P<K>::SK, n, C, v, s);
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
   // J stays one lane per handshake: at chunks <= 2^15 its launch, {J, decrypt core, SampleNTT}, is
@@ -2857,7 +2915,14 @@ size_t mlkem_scratch_bytes(const AlgInfo& a, size_t chunk) {
   return std::max(mlkem::scratch_words(a.k, C) * 8,
                   std::min(C, (size_t)QRK_KG_MULTI_MAX) * std::max(sizeof(mlkem::MkScr), sizeof(mlkem::PipeScr)));
 }
+size_t mlkem_matrix_bytes(const AlgInfo& a, size_t chunk) {
+  return (size_t)a.k * a.k * mlkem::round64(chunk) * mlkem::XOF_W * sizeof(uint64_t);
+}
 size_t mlkem_kg_flag_words() { return (size_t)QRK_KG_MULTI_MAX * mlkem::KG_FLAGS; }
+size_t mlkem_kg_scratch_bytes() {
+  return (size_t)QRK_KG_MULTI_MAX * std::max(sizeof(mlkem::MkScr), sizeof(mlkem::PipeScr));
+}
+int g_kg_dbg_late = -1;
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }

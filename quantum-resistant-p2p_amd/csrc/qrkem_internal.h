@@ -78,6 +78,13 @@ size_t mlkem_small_max();
 size_t mlkem_kg_multi_max();
 // flag / counter words of the single-shot multi-workgroup KeyGen (ctx->kg_cnt)
 size_t mlkem_kg_flag_words();
+// bytes of the batched sampled matrix of a chunk of `chunk` handshakes (Streams::xof_keep)
+size_t mlkem_matrix_bytes(const AlgInfo& a, size_t chunk);
+// bytes at the start of the scratch that the n <= mlkem_kg_multi_max() KeyGen kernels use
+size_t mlkem_kg_scratch_bytes();
+// tests only (qrk_dbg_kg_late): PRF item of k_keygen_pipe that publishes past every bounded wait,
+// -1 (default) none
+extern int g_kg_dbg_late;
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 
@@ -95,6 +102,10 @@ struct Streams {
   // per-handshake arrival counters of the multi-workgroup single-shot ML-KEM KeyGen (device,
   // QRK_KG_MULTI_MAX words, zero between calls: the last workgroup of a handshake resets its word)
   uint32_t* kg_cnt = nullptr;
+  // host-pointer ML-KEM KeyGen of n <= mlkem_kg_multi_max(): the call's error word (fine-grained host
+  // memory, device address, zeroed by the host before the launch).  When set, k_keygen_pipe runs and
+  // stores 1 there if a bounded cross-workgroup wait expired; the host then fails the call.
+  uint32_t* kg_err = nullptr;
   // single-shot ML-KEM (n == 1, host-pointer call): the public input in host memory (Encaps: pk;
   // Decaps: c), passed as a kernel argument instead of read over PCIe.  Secret inputs are never
   // passed by value: the runtime's kernel-argument pool is not wiped.
@@ -104,6 +115,12 @@ struct Streams {
   // and its first launch zeroes the other word, mlkem.hip rho_source)
   uint32_t* fixc = nullptr;
   int* fixp = nullptr;
+  // batched ML-KEM (one chunk, n > mlkem_small_max()), the handshake driver's expanded-key reuse:
+  // KeyGen writes its sampled matrix A_hat (SampleNTT(rho || x || y), the batched tiled layout,
+  // mlkem_matrix_bytes) to xof_keep instead of the scratch; Decaps of the same keys, same chunk size,
+  // takes it from xof_given and skips its own SampleNTT (A_hat is a function of rho alone).
+  uint64_t* xof_keep = nullptr;
+  const uint64_t* xof_given = nullptr;
 };
 
 // All pointers are device pointers; n handshakes processed as one chunk

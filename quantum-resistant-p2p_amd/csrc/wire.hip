@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __r
   uint32_t c = (uint32_t)(t0 % cpr);
   const size_t srec = S / cpr;
   const uint32_t sc = (uint32_t)(S % cpr);
+  const size_t nL = n * L;  // bytes in the input buffer
 #pragma unroll 1
   while (rec < n) {
     size_t r[ENC_U];
@@ -107,9 +108,10 @@ __global__ __launch_bounds__(256) void k_b64_encode(size_t n, const uint8_t* __r
       const uint32_t have = L - 12 * ch[u] < 12 ? L - 12 * ch[u] : 12;
       if (r[u] >= n) {
         w[u][0] = w[u][1] = w[u][2] = 0u;
-      } else if (((uintptr_t)src & 3) == 0 && (have == 12 || r[u] + 1 < n)) {
-        // a record's short last chunk reads into the next record (the same buffer) and masks those
-        // bytes off, so the wave never takes the byte-wise path for it
+      } else if (((uintptr_t)src & 3) == 0 && r[u] * L + 12 * ch[u] + 12 <= nL) {
+        // a record's short last chunk may read into the following records (the same buffer) and
+        // masks those bytes off, so the wave rarely takes the byte-wise path; the bound is the
+        // buffer's real end, since a short record (L < 12 - have) spans fewer than 12 bytes
         const uint3 v = *(const uint3*)src;
         w[u][0] = v.x, w[u][1] = v.y, w[u][2] = v.z;
 #pragma unroll
@@ -154,6 +156,7 @@ __global__ __launch_bounds__(256) void k_b64_decode(size_t n, const uint8_t* __r
   uint32_t c = (uint32_t)(t0 % cpr);
   const size_t srec = S / cpr;
   const uint32_t sc = (uint32_t)(S % cpr);
+  const size_t nIL = n * IL;  // characters in the input buffer
 #pragma unroll 1
   while (rec < n) {
     size_t r[DEC_U];
@@ -172,8 +175,9 @@ __global__ __launch_bounds__(256) void k_b64_decode(size_t n, const uint8_t* __r
       if (r[u] >= n) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) w[u][k] = 0u;
-      } else if (((uintptr_t)src & 3) == 0 && (nch == 16 || r[u] + 1 < n)) {
-        // a record's short last chunk reads into the next record; words past nch are never used
+      } else if (((uintptr_t)src & 3) == 0 && r[u] * IL + 16 * chs[u] + 16 <= nIL) {
+        // a record's short last chunk may read into the following records (never past the
+        // buffer's end); words past nch are never used
 #pragma unroll
         for (int k = 0; k < 4; ++k) w[u][k] = ((const uint32_t*)src)[k];
       } else {

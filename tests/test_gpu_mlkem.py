@@ -354,3 +354,39 @@ def test_fixup_counters_across_calls(alg, k):
         assert np.array_equal(ss[idx], oss), (step, n)
         # Decaps re-encrypts under the same fix-up-heavy rho (its implicit-rejection outcome as the oracle's)
         assert np.array_equal(ss2[idx], orc.batch_decaps(alg, sk[idx], np.ascontiguousarray(ct[idx]))), (step, n)
+
+
+@pytest.mark.parametrize("alg,item", [("ML-KEM-512", 0), ("ML-KEM-768", 0), ("ML-KEM-768", 5), ("ML-KEM-1024", 7)])
+def test_keygen_pipe_forced_timeout(engines, alg, item):
+    """The pipelined single-shot KeyGen (k_keygen_pipe, host-pointer calls of n <= 16) under a lost
+    hand-off: PRF item `item` publishes its NTT(s) / NTT(e) payload and flags 150 ms late, past every
+    consumer's and the collector's 50 ms bounded wait (debug knob qrk_dbg_kg_late).  The call must
+    fail (OQS_ERROR -> RuntimeError, as vendor/oqs.py:323-326 raises for the reference), never return
+    keys; the straggler's flags, set after the collector's reset, must not poison the next call,
+    which is byte-exact vs the oracle (single-shot and a 3-handshake host batch)."""
+    import ctypes as ct
+    import oracle as orc
+    from qrkem import oqs
+    from qrkem._native import LIB, last_error
+    dbg = LIB.qrk_dbg_kg_late
+    dbg.argtypes, dbg.restype = [ct.c_int], ct.c_int
+    rng = np.random.default_rng(item + 31 * len(alg))
+    kc = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    kcb = rng.integers(0, 256, (3, 64), dtype=np.uint8)
+    eng = engines[alg]
+    try:
+        dbg(item)
+        with pytest.raises(RuntimeError):
+            oqs.KeyEncapsulation(alg).generate_keypair_derand(kc)
+        with pytest.raises(RuntimeError):
+            eng.keypair(coins=kcb)
+        assert "hand-off timeout" in last_error()
+    finally:
+        dbg(-1)
+    opk, osk = orc.keypair(alg, kc)
+    for _ in range(2):
+        k = oqs.KeyEncapsulation(alg)
+        assert k.generate_keypair_derand(kc) == opk and k.export_secret_key() == osk
+        pk, sk = eng.keypair(coins=kcb)
+        bpk, bsk = orc.batch_keypair(alg, kcb)
+        assert np.array_equal(pk, bpk) and np.array_equal(sk, bsk)

@@ -74,3 +74,41 @@ def test_large_batch_roundtrip(codec):
     t = txt[idx].cpu().numpy()
     for a, b in zip(h, t):
         assert base64.b64encode(a.tobytes()) == b.tobytes()
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 5])
+def test_tight_hipmalloc_buffers(codec, L):
+    """records shorter than a 12-byte (16-character) chunk must not be loaded past the
+    end of the input.  The input here is a bare hipMalloc of exactly n*L bytes (n*IL characters),
+    not a torch tensor whose caching allocator pads the block, so the last records' chunks end at
+    the allocation's last byte."""
+    import ctypes as ct
+    import wire_spec
+    from qrkem._native import LIB
+    hip = ct.CDLL("libamdhip64.so")
+    n = 8191  # odd count: the last record's chunk is not 4-byte aligned for every L
+    rng = np.random.default_rng(100 + L)
+    data = rng.integers(0, 256, (n, L), dtype=np.uint8)
+    want_txt = wire_spec.encode_records(data)
+    IL = want_txt.shape[1]
+    pin, ptxt = ct.c_void_p(), ct.c_void_p()
+    assert hip.hipMalloc(ct.byref(pin), ct.c_size_t(n * L)) == 0
+    assert hip.hipMalloc(ct.byref(ptxt), ct.c_size_t(n * IL)) == 0
+    try:
+        assert hip.hipMemcpy(pin, data.ctypes.data_as(ct.c_void_p), ct.c_size_t(n * L), 1) == 0
+        assert hip.hipMemcpy(ptxt, want_txt.ctypes.data_as(ct.c_void_p), ct.c_size_t(n * IL), 1) == 0
+        txt = torch.empty((n, IL), dtype=torch.uint8, device="cuda")
+        back = torch.empty((n, L), dtype=torch.uint8, device="cuda")
+        st = torch.zeros((n,), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        s = ct.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert LIB.qrk_base64_encode_batch(codec._ctx, n, pin, L, ct.c_void_p(txt.data_ptr()), s) == 0
+        assert LIB.qrk_base64_decode_batch(codec._ctx, n, ptxt, L, ct.c_void_p(back.data_ptr()),
+                                           ct.c_void_p(st.data_ptr()), s) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(txt.cpu().numpy(), want_txt)
+        assert np.array_equal(back.cpu().numpy(), data)
+        assert int(st.abs().sum()) == 0
+    finally:
+        hip.hipFree(pin)
+        hip.hipFree(ptxt)
