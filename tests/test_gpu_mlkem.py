@@ -371,15 +371,17 @@ def test_keygen_pipe_forced_timeout(engines, alg, item):
     dbg = LIB.qrk_dbg_kg_late
     dbg.argtypes, dbg.restype = [ct.c_int], ct.c_int
     rng = np.random.default_rng(item + 31 * len(alg))
-    kc = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
-    kcb = rng.integers(0, 256, (3, 64), dtype=np.uint8)
+    kc, kc_lost = (rng.integers(0, 256, 64, dtype=np.uint8).tobytes() for _ in range(2))
+    kcb, kcb_lost = (rng.integers(0, 256, (3, 64), dtype=np.uint8) for _ in range(2))
     eng = engines[alg]
+    # the failing calls use other coins than the recovery calls, so a stale flag that let the next
+    # call read the straggler's payload would show up as wrong keys
     try:
         dbg(item)
         with pytest.raises(RuntimeError):
-            oqs.KeyEncapsulation(alg).generate_keypair_derand(kc)
+            oqs.KeyEncapsulation(alg).generate_keypair_derand(kc_lost)
         with pytest.raises(RuntimeError):
-            eng.keypair(coins=kcb)
+            eng.keypair(coins=kcb_lost)
         assert "hand-off timeout" in last_error()
     finally:
         dbg(-1)
