@@ -923,10 +923,11 @@ int qrk_ctx_staging_residue(qrk_ctx* ctx, uint64_t out[3]) {
   return 0;
 }
 
-// Tests only (not in qrkem.h): PRF item `item` of the pipelined single-shot ML-KEM KeyGen publishes
-// its payload and flags 150 ms late, past every bounded wait (-1: off).  Process-wide.
-extern "C" int qrk_dbg_kg_late(int item) {
-  g_kg_dbg_late = item;
+// Tests only (not in qrkem.h): the workgroup of role `role` of the pipelined single-shot ML-KEM KeyGen
+// (PRF item N = role < 2K, row r = role - 2K + 1) publishes its payload and flags 150 ms late, past
+// every bounded wait (-1: off).  Process-wide.
+extern "C" int qrk_dbg_kg_late(int role) {
+  g_kg_dbg_late = role;
   return 0;
 }
 

@@ -2260,9 +2260,14 @@ __device__ __forceinline__ uint32_t kg_pipe_pair(const PipeLds& sl, int p, BopAt
   const uint32_t t1 = (uint32_t)canon_f(acc_to_f(a1) + ef_at(2 * u + 1, L));
   return t0 | (t1 << 12);  // 24 bits, little-endian ek bytes 3p .. 3p + 2
 }
-// debug builds of a test: PRF item `late` (>= 0) sleeps this long before it stores its payload and
-// flags, past every consumer's and the collector's bounded wait (qrk_dbg_kg_late, tests only)
+// tests only (qrk_dbg_kg_late): the workgroup of role `late` (>= 0: PRF item N = role < 2K, or row
+// r = role - 2K + 1) sleeps this long before it stores its payload and flags, past every consumer's
+// and the collector's bounded wait
 constexpr uint64_t KG_DBG_LATE_TICKS = 15000000;  // 150 ms
+__device__ __forceinline__ void kg_dbg_sleep() {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < KG_DBG_LATE_TICKS) __builtin_amdgcn_s_sleep(127);
+}
 template <int K>
 __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const uint8_t* __restrict__ coins,
                                                               uint8_t* __restrict__ pk, uint8_t* __restrict__ sk,
@@ -2317,10 +2322,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         cbd_f<P<K>::ETA1>(f, cbd_load<P<K>::ETA1, 16>(sl.ps, (size_t)N, lane));
         contig_to_stride_f(f, (float*)sl.g.poly, lane);
         ntt_fwd_f<false>(f, (float*)sl.g.poly, lane);
-        if (N == late) {
-          const uint64_t t0 = wall_clock64();
-          while (wall_clock64() - t0 < KG_DBG_LATE_TICKS) __builtin_amdgcn_s_sleep(127);
-        }
+        if (role == late) kg_dbg_sleep();
         if (N < K) {
           const BOp b = make_bop_f(f, lane);
 #pragma unroll
@@ -2374,6 +2376,7 @@ __global__ __launch_bounds__(64 * (K + 2)) void k_keygen_pipe(size_t n, const ui
         io8[3 * p + 2] = (uint8_t)(tb[h] >> 16);
       }
       wave_phase();
+      if (role == late) kg_dbg_sleep();
       const uint32_t* io32 = (const uint32_t*)sl.io;
       for (int w = lane; w < 96; w += 64) st_sc1(&scr.th[r][w], io32[w]);
       kg_publish(&fl[8 + r]);
@@ -2761,7 +2764,11 @@ void launch_fix_prf(const uint8_t* rho, size_t n, size_t C, const ScratchView& v
 // launch-bound) costs more than the strided rho reads it saves (64 cache lines per wave instead of
 // 16; at 2^20 handshakes those reads were 1.2 GB per k_xof launch, see k_rho_copy).
 constexpr size_t DIRECT_RHO_MAX = (size_t)1 << 15;
-// Encaps / Decaps rho source for a chunk of C handshakes: keys_rho = the first key's rho
+// Encaps / Decaps rho source for a chunk of C handshakes: keys_rho = the first key's rho.
+// The fix-up counter pair is correct only because every batched ML-KEM Encaps / Decaps chunk reaches
+// this function through run_batch (abi.cpp), the only code that sets Streams::fixc / fixp, and
+// run_batch marks the pair dirty (both words re-zeroed before the next chunk) on any error after the
+// parity flip below.  A new caller of mlkem_encaps / mlkem_decaps must keep both properties.
 inline RhoSrc rho_source(const uint8_t* keys_rho, size_t key_stride, size_t n, size_t C, const ScratchView& v,
                          const Streams& s) {
   if (C <= DIRECT_RHO_MAX && s.fixc && s.fixp) {

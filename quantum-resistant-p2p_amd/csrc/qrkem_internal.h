@@ -82,8 +82,8 @@ size_t mlkem_kg_flag_words();
 size_t mlkem_matrix_bytes(const AlgInfo& a, size_t chunk);
 // bytes at the start of the scratch that the n <= mlkem_kg_multi_max() KeyGen kernels use
 size_t mlkem_kg_scratch_bytes();
-// tests only (qrk_dbg_kg_late): PRF item of k_keygen_pipe that publishes past every bounded wait,
-// -1 (default) none
+// tests only (qrk_dbg_kg_late): the k_keygen_pipe workgroup role (PRF item or t_hat row) that
+// publishes past every bounded wait, -1 (default) none
 extern int g_kg_dbg_late;
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
@@ -112,7 +112,8 @@ struct Streams {
   const uint8_t* host_in1 = nullptr;
   // batched ML-KEM Encaps / Decaps at chunks <= 2^15: the context's two SampleNTT fix-up counters
   // (device, zero at allocation) and which one the next call counts into (host; the call flips it
-  // and its first launch zeroes the other word, mlkem.hip rho_source)
+  // and its first launch zeroes the other word, mlkem.hip rho_source).  Set only by run_batch, which
+  // re-zeroes both words after any failed chunk (qrk_ctx::fixc_dirty).
   uint32_t* fixc = nullptr;
   int* fixp = nullptr;
   // batched ML-KEM (one chunk, n > mlkem_small_max()), the handshake driver's expanded-key reuse:

@@ -79,8 +79,9 @@ def test_tampered_implicit_rejection(engines, alg):
 @pytest.mark.parametrize("alg", ALGS)
 @pytest.mark.parametrize("n", [(1 << 15) - 5, (1 << 15) + 1])
 def test_pair_front_boundary(engines, alg, n):
-    """Chunks of at most 2^15 handshakes run the sponge fronts (H(ek) + G, J(z || c), G(m' || h))
-    on lane pairs (csrc/keccak_pair.cuh), larger chunks one lane per handshake: both sides of the
+    """Chunks of at most 2^15 handshakes run two sponge fronts, Encaps' H(ek) + G and Decaps'
+    G(m' || h), on lane pairs (csrc/keccak_pair.cuh; J(z || c) stays one lane per handshake), larger
+    chunks one lane per handshake: both sides of the
     boundary byte-exact vs the oracle on a sample of indices (both ends included), Decaps with a
     quarter of the ciphertexts tampered."""
     import oracle as orc
@@ -356,14 +357,18 @@ def test_fixup_counters_across_calls(alg, k):
         assert np.array_equal(ss2[idx], orc.batch_decaps(alg, sk[idx], np.ascontiguousarray(ct[idx]))), (step, n)
 
 
-@pytest.mark.parametrize("alg,item", [("ML-KEM-512", 0), ("ML-KEM-768", 0), ("ML-KEM-768", 5), ("ML-KEM-1024", 7)])
+# (alg, workgroup role): roles < 2K are PRF items (NTT(s_j) operands, NTT(e_i)), roles 2K .. 3K - 2 the
+# t_hat rows 1 .. K - 1, whose late t_hat flag the collector would otherwise take from the stale word
+@pytest.mark.parametrize("alg,item", [("ML-KEM-512", 0), ("ML-KEM-512", 4), ("ML-KEM-768", 0), ("ML-KEM-768", 5),
+                                      ("ML-KEM-768", 7), ("ML-KEM-1024", 7), ("ML-KEM-1024", 10)])
 def test_keygen_pipe_forced_timeout(engines, alg, item):
     """The pipelined single-shot KeyGen (k_keygen_pipe, host-pointer calls of n <= 16) under a lost
-    hand-off: PRF item `item` publishes its NTT(s) / NTT(e) payload and flags 150 ms late, past every
-    consumer's and the collector's 50 ms bounded wait (debug knob qrk_dbg_kg_late).  The call must
-    fail (OQS_ERROR -> RuntimeError, as vendor/oqs.py:323-326 raises for the reference), never return
-    keys; the straggler's flags, set after the collector's reset, must not poison the next call,
-    which is byte-exact vs the oracle (single-shot and a 3-handshake host batch)."""
+    hand-off: the workgroup of role `item` (a PRF item or a t_hat row) publishes its payload and flags
+    150 ms late, past every consumer's and the collector's 50 ms bounded wait (debug knob
+    qrk_dbg_kg_late).  The call must fail (OQS_ERROR -> RuntimeError, as vendor/oqs.py:323-326 raises
+    for the reference), never return keys; the straggler's flags, set after the collector's reset,
+    must not poison the next call, which is byte-exact vs the oracle (single-shot and a 3-handshake
+    host batch).  The row cases fail without the host's flag re-zeroing (profiles/r6/single_shot/)."""
     import ctypes as ct
     import oracle as orc
     from qrkem import oqs

@@ -20,3 +20,4 @@ for l in open(sys.argv[1]):
     print(d['variant'], 'oqs_keypair', s['oqs_keypair'], 'host_keypair', s['host_keypair'], 'oqs_enc', s['oqs_encaps'], 'oqs_dec', s['oqs_decaps'])
 PY
 abx 3 hs_r6=default hs_r5=r5pipe -- --mode handshake --steps 10 --warmup 3 && cat $O/abx.jsonl | cut -c1-120
+probe ss_service ss_service_probe.hip && cat $O/ss_service.txt
