@@ -2633,9 +2633,13 @@ struct RDecrypt {  // m' = K-PKE.Decrypt(dk, c), 16 lanes / handshake
   }
 };
 
+// Waves per SIMD the core is compiled for: 3 (<= 168 VGPRs).  ML-KEM-1024's Decaps core spills at
+// 168 (16 B) and takes a scratch allocation that slowed the launch after it, so it keeps its 176
+// VGPRs (2 waves); its Encaps core fits 168 without spilling: 3.05 -> 2.77 ms per 2^20 core launch
+// (both cores at 3 waves, profiles/r6/core4/).
 template <int K, int MODE>
 struct RCore {  // K-PKE.Encrypt (MODE 1: the Decaps re-encryption, compare and select), 16 lanes / hs
-  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = K == 4 ? 1 : 3;
+  static constexpr int LDS = GROUPS * (int)sizeof(GroupLds), WPE = (K == 4 && MODE == 1) ? 1 : 3;
   size_t n, C;
   const uint64_t *xof, *prf;
   const uint8_t* ek;
