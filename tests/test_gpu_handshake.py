@@ -92,23 +92,25 @@ def test_key_derivation_host_inputs(kdf):
         assert out[i].tobytes() == hkdf_spec.hkdf_sha256(ss[i], info, 32)
 
 
-@pytest.mark.parametrize("alg", ["ML-KEM-512", "ML-KEM-768", "ML-KEM-1024"])
-def test_handshake_driver_expanded_key_reuse_matches_oracle(alg):
+@pytest.mark.parametrize("alg,n,chunk", [("ML-KEM-512", 3000, 2048), ("ML-KEM-768", 3000, 2048),
+                                         ("ML-KEM-1024", 3000, 2048), ("ML-KEM-768", 1089, 1088)])
+def test_handshake_driver_expanded_key_reuse_matches_oracle(alg, n, chunk):
     """Batched ML-KEM chunks (> 1024 handshakes) keep the initiator's sampled matrix A_hat from its
     KeyGen (messaging.py:590) for its Decaps (:1038) instead of re-running SampleNTT; the last chunk
-    here (952) runs the one-launch kernels without reuse.  Every output byte-exact vs the oracle's
+    (952, or a single handshake) runs the one-launch kernels without reuse; 1088 is the first
+    batched chunk size, a ragged 64-handshake tile.  Every output byte-exact vs the oracle's
     handshake (a wrong A_hat would re-encrypt differently and select the implicit-rejection key)."""
     import oracle as orc
     import hkdf_spec
     from make_golden_handshake import node_id
     from qrkem.handshake import HandshakeDriver
-    n, sym = 3000, "AES-256-GCM"
+    sym = "AES-256-GCM"
     s = orc.sizes(alg)
     kp, enc = s["keypair_coins"], s["encaps_coins"]
     coins = orc.bench_coins(n, 2 * kp + enc, seed=0xA11 + kp)
     kpi, kpr, en = (np.ascontiguousarray(coins[:, a:b]) for a, b in ((0, kp), (kp, 2 * kp), (2 * kp, 2 * kp + enc)))
     infos = [hkdf_spec.protocol_info(node_id(b"a", i), node_id(b"b", i), sym) for i in range(n)]
-    drv = HandshakeDriver(alg, symmetric_name=sym, chunk=2048)
+    drv = HandshakeDriver(alg, symmetric_name=sym, chunk=chunk)
     out = drv.run(infos, coins_kp_initiator=kpi, coins_kp_responder=kpr, coins_encaps=en)
     torch.cuda.synchronize()
     want = orc.batch_handshake(alg, kpi, kpr, en, infos, hkdf_spec.SYMMETRIC_KEY_SIZE[sym])

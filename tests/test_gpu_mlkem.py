@@ -105,10 +105,13 @@ def test_pair_front_boundary(engines, alg, n):
 
 
 @pytest.mark.parametrize("alg", ALGS)
-def test_host_pointer_api(engines, alg):
+@pytest.mark.parametrize("n", [5, 16, 17])
+def test_host_pointer_api(engines, alg, n):
+    """Host-array calls: n <= 16 KeyGens run the pipelined kernel (k_keygen_pipe, its error word
+    checked), n = 17 the one-workgroup-per-handshake kernel; Encaps / Decaps the one-launch kernels."""
     import oracle as orc
     eng = engines[alg]
-    coins = orc.bench_coins(5, 96, seed=5)
+    coins = orc.bench_coins(n, 96, seed=5 + n)
     kc, ec = np.ascontiguousarray(coins[:, :64]), np.ascontiguousarray(coins[:, 64:])
     pk, sk = eng.keypair(coins=kc)
     ct, ss, st = eng.encaps(pk, coins=ec, return_status=True)
