@@ -10,6 +10,7 @@ import sys
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "quantum-resistant-p2p_amd"))
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from qrkem._native import LIB  # noqa: E402
 from qrkem.batch import BatchKEM  # noqa: E402
@@ -19,7 +20,7 @@ fn = LIB.qrk_dbg_ss_trace
 fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 MARKS = {
     # k_keygen_multi (n = 1): one workgroup per PRF / SampleNTT item, the last to count in finishes
-    # k_keygen_pipe (n = 1, the default): t = 0 is the collector workgroup's start
+    # k_keygen_pipe (n = 1 host-pointer calls, the default there): t = 0 is the collector workgroup's start
     "keypair": {1: "PRF item 0 published", 7: "H wave: G done", 10: "SampleNTT A[0][0] block 1",
                 11: "block 2", 12: "block 3", 2: "A[0][0] done", 22: "t wave: s_hat, e_hat loaded",
                 8: "H block 0 starts", 13: "H block 1 starts", 9: "H block 2 starts", 14: "H block 3 starts",
@@ -46,8 +47,8 @@ for op in ("keypair", "encaps", "decaps"):
     acc = {k: [] for k in MARKS[op]}
     mhz = []
     for _ in range(N):
-        if op == "keypair":
-            eng.keypair(n=1)
+        if op == "keypair":  # host coins: the host-pointer path runs the pipelined KeyGen (k_keygen_pipe)
+            eng.keypair(coins=np.random.default_rng(_).integers(0, 256, (1, 64), dtype=np.uint8))
         elif op == "encaps":
             eng.encaps(pk)
         else:
