@@ -258,23 +258,25 @@ def test_large_batch_roundtrip_and_sample(engines):
     assert np.array_equal(ct_h, oct_) and np.array_equal(ss_h, oss)
 
 
-def test_kat_records_through_single_shot_wrapper(golden_dir):
+@pytest.mark.parametrize("alg", ALGS)
+def test_kat_records_through_single_shot_wrapper(golden_dir, alg):
     """BASELINE.json configs[0] as the reference runs it: one KEM object and one call per
     handshake through the oqs-compatible wrapper (qrkem.oqs, the drop-in for vendor/oqs.py),
-    1024 NIST-KAT-DRBG records of ML-KEM-768, digests equal to the golden ones."""
+    every NIST-KAT-DRBG record (1024 for ML-KEM-768), digests equal to the golden ones; KeyGen
+    runs the pipelined single-shot kernel (k_keygen_pipe), Encaps / Decaps the one-launch kernels."""
     import json
     import oracle as orc
     from qrkem import oqs
-    g = json.loads((golden_dir / "kat_mlkem.json").read_text())["ML-KEM-768"]
+    g = json.loads((golden_dir / "kat_mlkem.json").read_text())[alg]
     n = g["count"]
     _, kc, ec = orc.kat_coins(n, 64, 32)
     h = {k: hashlib.sha256() for k in ("pk", "sk", "ct", "ss")}
     for i in range(n):
-        kem = oqs.KeyEncapsulation("ML-KEM-768")
+        kem = oqs.KeyEncapsulation(alg)
         pk = kem.generate_keypair_derand(kc[i].tobytes())
         sk = kem.export_secret_key()
-        c, ss = oqs.KeyEncapsulation("ML-KEM-768").encap_secret_derand(pk, ec[i].tobytes())
-        assert oqs.KeyEncapsulation("ML-KEM-768", sk).decap_secret(c) == ss
+        c, ss = oqs.KeyEncapsulation(alg).encap_secret_derand(pk, ec[i].tobytes())
+        assert oqs.KeyEncapsulation(alg, sk).decap_secret(c) == ss
         for k, v in (("pk", pk), ("sk", sk), ("ct", c), ("ss", ss)):
             h[k].update(v)
     for k in h:
