@@ -931,6 +931,22 @@ extern "C" int qrk_dbg_kg_late(int role) {
   return 0;
 }
 
+// Tests only (not in qrkem.h): nonzero words among the context's single-shot KeyGen flag / counter
+// words, which must be zero between calls (after a failed pipelined KeyGen too).
+extern "C" int qrk_dbg_kg_flags_residue(qrk_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return fail("null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  ctx_quiesce(ctx);
+  *out = 0;
+  if (!ctx->kg_cnt) return 0;
+  std::vector<uint32_t> tmp(mlkem_kg_flag_words());
+  const hipError_t e = hipMemcpy(tmp.data(), ctx->kg_cnt, tmp.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  for (uint32_t x : tmp) *out += x != 0;
+  return e == hipSuccess ? 0 : hip_fail("hipMemcpy(kg flags)", e);
+}
+
 // Tests only (not in qrkem.h): nonzero bytes left in the ML-KEM per-handshake records of a chunk
 // of n handshakes (mlkem_cleanse wipes them after every chunk).
 extern "C" int qrk_dbg_mlkem_records_residue(qrk_ctx* ctx, const char* alg, size_t n, uint64_t* out) {

@@ -373,7 +373,8 @@ def test_keygen_pipe_forced_timeout(engines, alg, item):
     qrk_dbg_kg_late).  The call must fail (OQS_ERROR -> RuntimeError, as vendor/oqs.py:323-326 raises
     for the reference), never return keys; the straggler's flags, set after the collector's reset,
     must not poison the next call, which is byte-exact vs the oracle (single-shot and a 3-handshake
-    host batch).  The row cases fail without the host's flag re-zeroing (profiles/r6/single_shot/)."""
+    host batch), and the context's flag words are all zero again after the failed call (a build
+    without the host's re-zeroing leaves the straggler's flags set, profiles/r6/single_shot/)."""
     import ctypes as ct
     import oracle as orc
     from qrkem import oqs
@@ -393,6 +394,11 @@ def test_keygen_pipe_forced_timeout(engines, alg, item):
         with pytest.raises(RuntimeError):
             eng.keypair(coins=kcb_lost)
         assert "hand-off timeout" in last_error()
+        # the straggler set its flags after the collector's reset; the failed call re-zeroed them
+        res = LIB.qrk_dbg_kg_flags_residue
+        res.argtypes, res.restype = [ct.c_void_p, ct.POINTER(ct.c_uint64)], ct.c_int
+        cnt = ct.c_uint64(1)
+        assert res(eng._ctx, ct.byref(cnt)) == 0 and cnt.value == 0
     finally:
         dbg(-1)
     opk, osk = orc.keypair(alg, kc)
