@@ -931,6 +931,26 @@ extern "C" int qrk_dbg_kg_late(int role) {
   return 0;
 }
 
+// Tests only (not in qrkem.h): batched ML-KEM Encaps / Decaps chunks of at most 2^15 handshakes fail
+// right after the SampleNTT fix-up counter parity flip, before their first launch (0: off), and the
+// context's two fix-up counter words and its parity read back (the re-zero path).
+extern "C" int qrk_dbg_fail_after_flip(int on) {
+  g_dbg_fail_after_flip = on;
+  return 0;
+}
+extern "C" int qrk_dbg_fixc_words(qrk_ctx* ctx, uint32_t* out, int* parity) {
+  if (!ctx || !out || !parity) return fail("null argument");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard device_guard;
+  if (device_guard.set(ctx->device)) return -1;
+  ctx_quiesce(ctx);
+  out[0] = out[1] = 0;
+  *parity = ctx->fixp;
+  if (!ctx->fixc) return 0;
+  const hipError_t e = hipMemcpy(out, ctx->fixc, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : hip_fail("hipMemcpy(fixc)", e);
+}
+
 // Tests only (not in qrkem.h): nonzero words among the context's single-shot KeyGen flag / counter
 // words, which must be zero between calls (after a failed pipelined KeyGen too).
 extern "C" int qrk_dbg_kg_flags_residue(qrk_ctx* ctx, uint64_t* out) {

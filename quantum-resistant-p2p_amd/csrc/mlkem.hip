@@ -2778,6 +2778,7 @@ inline RhoSrc rho_source(const uint8_t* keys_rho, size_t key_stride, size_t n, s
   if (C <= DIRECT_RHO_MAX && s.fixc && s.fixp) {
     const int p = *s.fixp;
     *s.fixp = p ^ 1;  // the next call counts into the word this call's main pass zeroes
+    if (g_dbg_fail_after_flip) qrk_chk(hipErrorLaunchFailure);  // tests only: a failure after the flip
     return {keys_rho, key_stride, s.fixc + p, s.fixc + (p ^ 1)};
   }
   // k_xof reads rho from the compact copy in scratch
@@ -2850,6 +2851,7 @@ hipError_t encaps_impl(size_t n, uint8_t* ct, uint8_t* ss, const uint8_t* pk, co
   hipStream_t st = s.main;
   poison_xof<K>(C, v, st);
   const RhoSrc rho = rho_source(pk + 384 * K, (size_t)P<K>::PK, n, C, v, s);
+  if (g_launch_err != hipSuccess) return g_launch_err;  // nothing after a failed step
   const RFrontEnc<K> front{pk, coins, n, ss, v.seeds, blocks_for(n)};
   const RPrf<P<K>::ETA1, P<K>::ETA2> prf{v.seeds, n, C, 2 * K + 1, K, v.prf, blocks_for((2 * K + 1) * C)};
   const RCore<K, 0> core{n, C, v.xof, v.prf, pk, (size_t)P<K>::PK, coins, (size_t)32, ct, status, v.kprime, v.kbar,
@@ -2899,6 +2901,7 @@ hipError_t decaps_impl(size_t n, uint8_t* ss, const uint8_t* ct, const uint8_t* 
   }
   poison_xof<K>(C, v, st);
   const RhoSrc rho = rho_source(sk + 768 * K, (size_t)P<K>::SK, n, C, v, s);
+  if (g_launch_err != hipSuccess) return g_launch_err;  // nothing after a failed step
   const RCore<K, 1> core{n, C, v.xof, v.prf, sk + 384 * K, (size_t)P<K>::SK, (const uint8_t*)v.mprime, (size_t)32,
                          const_cast<uint8_t*>(ct), nullptr, v.kprime, v.kbar, ss, gblocks};
   // J stays one lane per handshake: at chunks <= 2^15 its launch, {J, decrypt core, SampleNTT}, is
@@ -2934,6 +2937,7 @@ size_t mlkem_kg_scratch_bytes() {
   return (size_t)QRK_KG_MULTI_MAX * std::max(sizeof(mlkem::MkScr), sizeof(mlkem::PipeScr));
 }
 int g_kg_dbg_late = -1;
+int g_dbg_fail_after_flip = 0;
 
 size_t mlkem_small_max() { return QRK_SMALL_MAX; }
 size_t mlkem_kg_multi_max() { return QRK_KG_MULTI_MAX; }

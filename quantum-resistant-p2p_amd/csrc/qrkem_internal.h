@@ -85,6 +85,9 @@ size_t mlkem_kg_scratch_bytes();
 // tests only (qrk_dbg_kg_late): the k_keygen_pipe workgroup role (PRF item or t_hat row) that
 // publishes past every bounded wait, -1 (default) none
 extern int g_kg_dbg_late;
+// tests only (qrk_dbg_fail_after_flip): batched ML-KEM Encaps / Decaps chunks <= 2^15 fail right after
+// the fix-up counter parity flip, before any launch (0 = off)
+extern int g_dbg_fail_after_flip;
 hipError_t frodo_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 hipError_t hqc_cleanse(const AlgInfo& a, size_t n, void* scratch, hipStream_t st);
 

@@ -408,3 +408,65 @@ def test_keygen_pipe_forced_timeout(engines, alg, item):
         pk, sk = eng.keypair(coins=kcb)
         bpk, bsk = orc.batch_keypair(alg, kcb)
         assert np.array_equal(pk, bpk) and np.array_equal(sk, bsk)
+
+
+@pytest.mark.parametrize("op", ["encaps", "decaps"])
+def test_fixup_counters_rezeroed_after_failed_chunk(op):
+    """the two alternating SampleNTT fix-up counters of chunks <= 2^15 stay exact when a
+    chunk fails after the parity flip (debug hook qrk_dbg_fail_after_flip: the chunk returns an
+    error before its first launch, so its main pass never zeroes the word the next call counts
+    into).  The failed call raises; the next call counts exactly n x (its pk's fix-up entries) --
+    read back with qrk_dbg_fixc_words -- and is byte-exact vs the oracle.  Without the re-zero the
+    word would carry the previous call's count as well."""
+    import ctypes as ct
+    import oracle as orc
+    from qrkem._native import LIB
+    from qrkem.batch import BatchKEM
+    alg, k = "ML-KEM-768", 3
+    rng = np.random.default_rng(1234)
+    for _ in range(4000):
+        rho = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        bad = sum(_sample_ntt_needs_4th_block(rho, i, j) for i in range(k) for j in range(k))
+        if bad >= 1:
+            break
+    else:
+        pytest.fail("no rho with a 4-block SampleNTT entry found")
+    kc0 = np.ascontiguousarray(orc.bench_coins(1, 64, seed=1234))
+    opk, osk = orc.batch_keypair(alg, kc0)
+    opk[:, -32:] = np.frombuffer(rho, dtype=np.uint8)
+    osk[:, 768 * k:768 * k + 32] = np.frombuffer(rho, dtype=np.uint8)
+    fail = LIB.qrk_dbg_fail_after_flip
+    fail.argtypes, fail.restype = [ct.c_int], ct.c_int
+    words = LIB.qrk_dbg_fixc_words
+    words.argtypes, words.restype = [ct.c_void_p, ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_int)], ct.c_int
+    eng = BatchKEM(alg, device=0)
+
+    def run(n, seed):
+        coins = orc.bench_coins(n, 32, seed=seed)
+        pk, sk = np.repeat(opk, n, axis=0), np.repeat(osk, n, axis=0)
+        if op == "encaps":
+            ct_, ss = eng.encaps(_dev(pk), coins=_dev(coins))
+            return pk, sk, coins, _host(ct_), _host(ss)
+        oct_, _ = orc.batch_encaps(alg, pk, coins)
+        return pk, sk, coins, oct_, _host(eng.decaps(_dev(sk), _dev(oct_)))
+
+    run(1100, 1)  # counts 1100 * bad into one word
+    try:
+        fail(1)
+        with pytest.raises(RuntimeError):
+            run(1200, 2)
+    finally:
+        fail(0)
+    n = 1300
+    pk, sk, coins, ct_, ss = run(n, 3)
+    w = (ct.c_uint32 * 2)()
+    par = ct.c_int()
+    assert words(eng._ctx, w, ct.byref(par)) == 0
+    assert sorted([w[0], w[1]]) == [0, n * bad], (w[0], w[1], bad)
+    idx = np.unique(np.r_[np.arange(4), np.linspace(0, n - 1, 60).astype(int)])
+    if op == "encaps":
+        oct_, oss = orc.batch_encaps(alg, pk[idx], np.ascontiguousarray(coins[idx]))
+        assert np.array_equal(ct_[idx], oct_) and np.array_equal(ss[idx], oss)
+    else:
+        assert np.array_equal(ss[idx], orc.batch_decaps(alg, sk[idx], np.ascontiguousarray(ct_[idx])))
+    eng.close()
