@@ -96,6 +96,51 @@ def test_device_keypair_then_frodo_host_encaps_without_sync():
     assert np.array_equal(sk.index_select(0, ti).cpu().numpy(), osk)
 
 
+def test_host_single_shot_then_device_calls_without_sync():
+    """Host-pointer calls run on the context's I/O stream, device-pointer calls on the torch
+    stream; each waits for the other through the context's last-use event (abi.cpp LastUse /
+    ctx_order).  Single-shot host calls (the pipelined KeyGen uses the context scratch)
+    interleaved with device-pointer calls, no synchronize in between, then a host batch large
+    enough to regrow the pinned mirror (ctx_quiesce): every output byte-exact vs the oracle."""
+    import oracle as orc
+    from qrkem.batch import BatchKEM
+    n = 1 << 13
+    eng = BatchKEM(ALG, device=0)
+    for it in range(3):
+        kc = np.ascontiguousarray(orc.bench_coins(1, 64, seed=300 + it))
+        ec = np.ascontiguousarray(orc.bench_coins(1, 32, seed=310 + it))
+        dkc = orc.bench_coins(n, 96, seed=320 + it)
+        d_kc = torch.from_numpy(np.ascontiguousarray(dkc[:, :64])).cuda()
+        d_ec = torch.from_numpy(np.ascontiguousarray(dkc[:, 64:])).cuda()
+        torch.cuda.synchronize()
+        hpk, hsk = eng.keypair(coins=kc)            # host, n = 1: I/O stream, context scratch
+        pk, sk = eng.keypair(coins=d_kc)            # torch stream, same scratch
+        hct, hss = eng.encaps(hpk, coins=ec)        # host single-shot again
+        ct_, ss = eng.encaps(pk, coins=d_ec)        # torch stream
+        hss2 = eng.decaps(hsk, hct)                 # host single-shot
+        ss2 = eng.decaps(sk, ct_)                   # torch stream
+        torch.cuda.synchronize()
+        opk, osk = orc.batch_keypair(ALG, kc)
+        oct_, oss = orc.batch_encaps(ALG, opk, ec)
+        assert np.array_equal(hpk, opk) and np.array_equal(hsk, osk)
+        assert np.array_equal(hct, oct_) and np.array_equal(hss, oss) and np.array_equal(hss2, oss)
+        assert torch.equal(ss, ss2)
+        idx = np.unique(np.r_[0:4, 0:n:509, n - 4:n])
+        ti = torch.from_numpy(idx).cuda()
+        dpk, dsk = orc.batch_keypair(ALG, np.ascontiguousarray(dkc[idx, :64]))
+        dct, dss = orc.batch_encaps(ALG, dpk, np.ascontiguousarray(dkc[idx, 64:]))
+        assert np.array_equal(sk.index_select(0, ti).cpu().numpy(), dsk)
+        assert np.array_equal(ct_.index_select(0, ti).cpu().numpy(), dct)
+        assert np.array_equal(ss2.index_select(0, ti).cpu().numpy(), dss)
+    # a host batch of 3000 regrows the pinned I/O mirror (waits for the last use first)
+    m = 3000
+    c3 = orc.bench_coins(m, 96, seed=330)
+    pk3, sk3 = eng.keypair(coins=np.ascontiguousarray(c3[:, :64]))
+    sel = np.r_[0:3, m - 3:m]
+    opk3, osk3 = orc.batch_keypair(ALG, np.ascontiguousarray(c3[sel, :64]))
+    assert np.array_equal(pk3[sel], opk3) and np.array_equal(sk3[sel], osk3)
+
+
 def _residue(ctx):
     import ctypes as ct
     from qrkem._native import LIB
