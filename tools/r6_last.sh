@@ -1,7 +1,7 @@
 # round 6, last check of HEAD: the whole GPU suite, smoke, the default bench line, and a two-rank
 # rehearsal of the multi-GPU bench path on this one GPU (gloo for the reduce, both ranks on cuda:0)
 set -o pipefail
-cd /root/repo && source tools/gpu.sh && out r6/last2
+cd /root/repo && source tools/gpu.sh && out r6/last3
 SUITE_TIMEOUT=1500 suite tests || exit 1
 smoke || exit 1
 bench bench_default && cut -c1-200 $O/bench_default.json || exit 1
